@@ -1,0 +1,355 @@
+"""Spark-shaped `ALS` estimator and `ALSModel` over libalbedo_als.so.
+
+Mirrors the surface albedo's jobs use:
+  * ALSRecommenderBuilder.scala:46-58 / Playground.scala:54-65 / train_als.py:55-61:
+      ALS().setImplicitPrefs(True).setRank(50).setRegParam(0.5).setAlpha(40).setMaxIter(26)
+           .setSeed(42).setColdStartStrategy("drop").setUserCol(..).setItemCol(..)
+           .setRatingCol(..).fit(dataset)
+  * ALSRecommender.scala:16-19,33-36 reads model.userFactors / model.itemFactors / model.rank
+  * ALSRecommender.scala:28-65 (+ BoundedPriorityQueue.scala:30-53) is recommendForUserSubset
+  * LogisticRegressionRanker.scala:167-174,229 uses model.transform (coldStartStrategy drop)
+  * ModelUtils.scala:7-20 persists with model.write.overwrite().save(path) / ALSModel.load(path)
+Parameter names, defaults and validation messages follow Spark 2.2.0's ALSParams.  Datasets are
+pandas DataFrames or dicts of arrays (there is no JVM here); outputs are pandas DataFrames.
+All compute runs on the MI355X through the C ABI; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import time
+
+import numpy as np
+
+from . import _lib
+from ._lib import IllegalArgumentException, check, load, ptr
+
+SPARK_DEFAULT_SEED = 1994790107  # "org.apache.spark.ml.recommendation.ALS".hashCode (ALS setDefault(seed))
+
+
+def _column(dataset, name):
+    if dataset is None:
+        raise IllegalArgumentException(_lib.ALS_E_INVALID_ARGUMENT, "dataset is None")
+    try:
+        col = dataset[name]
+    except (KeyError, IndexError, TypeError):
+        raise IllegalArgumentException(_lib.ALS_E_INVALID_ARGUMENT, f"Field \"{name}\" does not exist.") from None
+    return np.asarray(col)
+
+
+def _checked_cast(values, col):
+    """ALS.checkedCast: ids must be numeric and within Int range (Spark 2.2.0 error messages)."""
+    v = np.asarray(values)
+    if v.dtype.kind not in "iuf":
+        raise IllegalArgumentException(_lib.ALS_E_INVALID_ARGUMENT,
+                                       f"ALS only supports values in Integer range for column {col}. "
+                                       f"Column {col} was not numeric.")
+    if v.size == 0:
+        return v.astype(np.int32)
+    if v.dtype.kind == "f":
+        bad = (v != np.floor(v)) | (v < -2**31) | (v > 2**31 - 1) | ~np.isfinite(v)
+    else:
+        bad = (v < -2**31) | (v > 2**31 - 1)
+    if np.any(bad):
+        x = v[np.argmax(bad)]
+        raise IllegalArgumentException(_lib.ALS_E_INVALID_ARGUMENT,
+                                       f"ALS only supports values in Integer range and without fractional part "
+                                       f"for columns {col}. Value {x} was either out of Integer range or "
+                                       f"contained a fractional part that could not be converted.")
+    return v.astype(np.int32)
+
+
+class _Params:
+    _defaults = dict(rank=10, maxIter=10, regParam=0.1, numUserBlocks=10, numItemBlocks=10,
+                     implicitPrefs=False, alpha=1.0, userCol="user", itemCol="item",
+                     ratingCol="rating", predictionCol="prediction", seed=SPARK_DEFAULT_SEED,
+                     nonnegative=False, checkpointInterval=10, coldStartStrategy="nan",
+                     intermediateStorageLevel="MEMORY_AND_DISK", finalStorageLevel="MEMORY_AND_DISK",
+                     device=-1, lightMaxDegree=-1)
+    _doc = dict(rank="rank of the factorization", maxIter="max number of iterations (>= 0)",
+                regParam="regularization parameter (>= 0)", alpha="alpha for implicit preference",
+                implicitPrefs="whether to use implicit preference", nonnegative="whether to use nonnegative constraint for least squares",
+                coldStartStrategy="strategy for dealing with unknown or new users/items at prediction time: nan, drop",
+                seed="random seed", numUserBlocks="number of user blocks", numItemBlocks="number of item blocks",
+                userCol="column name for user ids", itemCol="column name for item ids",
+                ratingCol="column name for ratings", predictionCol="prediction column name",
+                checkpointInterval="checkpoint interval (kept for API parity; factors stay resident in HBM)",
+                intermediateStorageLevel="kept for API parity", finalStorageLevel="kept for API parity",
+                device="HIP device ordinal (-1 = current)",
+                lightMaxDegree="rows with <= this many ratings use the push-through solve (-1 default, 0 off)")
+
+    def __init__(self, **kw):
+        self._p = dict(self._defaults)
+        for k, v in kw.items():
+            self._set(k, v)
+
+    def _set(self, k, v):
+        if k not in self._defaults:
+            raise IllegalArgumentException(_lib.ALS_E_INVALID_ARGUMENT, f"unknown param {k}")
+        if k == "coldStartStrategy":
+            v = str(v).lower()
+            if v not in ("nan", "drop"):
+                raise IllegalArgumentException(_lib.ALS_E_INVALID_ARGUMENT,
+                                               f"als parameter coldStartStrategy given invalid value {v}.")
+        if k == "checkpointInterval" and not (v == -1 or v >= 1):
+            raise IllegalArgumentException(_lib.ALS_E_INVALID_ARGUMENT,
+                                           f"als parameter checkpointInterval given invalid value {v}.")
+        self._p[k] = v
+        return self
+
+    def explainParams(self) -> str:
+        lines = []
+        for k in self._defaults:
+            cur = self._p[k]
+            dft = self._defaults[k]
+            extra = f"(default: {dft}" + (f", current: {cur})" if cur != dft else ")")
+            lines.append(f"{k}: {self._doc.get(k, '')} {extra}")
+        return "\n".join(lines)
+
+
+def _make_accessors(cls):
+    for k in _Params._defaults:
+        cap = k[0].upper() + k[1:]
+        setattr(cls, "set" + cap, (lambda key: lambda self, v: self._set(key, v))(k))
+        setattr(cls, "get" + cap, (lambda key: lambda self: self._p[key])(k))
+    return cls
+
+
+@_make_accessors
+class ALS(_Params):
+    """Spark ml.recommendation.ALS (estimator)."""
+
+    def _c_params(self):
+        p = _lib.als_params()
+        check(load().als_params_default(C.byref(p)))
+        p.rank = int(self._p["rank"])
+        p.max_iter = int(self._p["maxIter"])
+        p.implicit_prefs = 1 if self._p["implicitPrefs"] else 0
+        p.nonnegative = 1 if self._p["nonnegative"] else 0
+        p.num_user_blocks = int(self._p["numUserBlocks"])
+        p.num_item_blocks = int(self._p["numItemBlocks"])
+        p.reg_param = float(self._p["regParam"])
+        p.alpha = float(self._p["alpha"])
+        p.seed = int(self._p["seed"])
+        p.device = int(self._p["device"])
+        p.light_max_degree = int(self._p["lightMaxDegree"])
+        return p
+
+    def _context(self):
+        lib = load()
+        p = self._c_params()
+        h = C.c_void_p()
+        check(lib.als_create(C.byref(p), C.byref(h)))
+        return h
+
+    def fit(self, dataset, initialUserFactors=None, initialItemFactors=None) -> "ALSModel":
+        """ALS.fit. `initial*Factors` = (ids, factors[n, rank]) injects the start point (parity path);
+        without it the Spark-style XORShiftRandom initialisation is used."""
+        user = _checked_cast(_column(dataset, self._p["userCol"]), self._p["userCol"])
+        item = _checked_cast(_column(dataset, self._p["itemCol"]), self._p["itemCol"])
+        rating = np.ascontiguousarray(_column(dataset, self._p["ratingCol"]), dtype=np.float32)
+        if user.size == 0:
+            raise IllegalArgumentException(_lib.ALS_E_INVALID_ARGUMENT,
+                                           "No ratings available from the input dataset.")
+        lib = load()
+        h = self._context()
+        try:
+            user = np.ascontiguousarray(user)
+            item = np.ascontiguousarray(item)
+            check(lib.als_set_ratings(h, user.size, ptr(user, C.c_int32), ptr(item, C.c_int32),
+                                      ptr(rating, C.c_float)))
+            for side, init in ((_lib.ALS_USER, initialUserFactors), (_lib.ALS_ITEM, initialItemFactors)):
+                if init is not None:
+                    ids = np.ascontiguousarray(init[0], dtype=np.int32)
+                    f = np.ascontiguousarray(init[1], dtype=np.float32)
+                    check(lib.als_set_initial_factors(h, side, ids.size, ptr(ids, C.c_int32), ptr(f, C.c_float)))
+            t0 = time.perf_counter()
+            check(lib.als_fit(h))
+            fit_s = time.perf_counter() - t0
+        except Exception:
+            lib.als_destroy(h)
+            raise
+        model = ALSModel(h, dict(self._p))
+        model.fit_seconds = fit_s
+        return model
+
+
+@_make_accessors
+class ALSModel(_Params):
+    """Spark ml.recommendation.ALSModel over an engine context holding both factor matrices."""
+
+    def __init__(self, handle, params):
+        super().__init__()
+        self._p.update(params)
+        self._h = handle
+        self._cache = {}
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            try:
+                load().als_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    @property
+    def rank(self) -> int:
+        return int(load().als_rank(self._h))
+
+    def _factors(self, side):
+        if side not in self._cache:
+            lib = load()
+            n = lib.als_num_rows(self._h, side)
+            ids = np.empty(n, dtype=np.int32)
+            f = np.empty((n, self.rank), dtype=np.float32)
+            check(lib.als_get_factors(self._h, side, ptr(ids, C.c_int32), ptr(f, C.c_float)))
+            self._cache[side] = (ids, f)
+        return self._cache[side]
+
+    def user_factors_np(self):
+        return self._factors(_lib.ALS_USER)
+
+    def item_factors_np(self):
+        return self._factors(_lib.ALS_ITEM)
+
+    @staticmethod
+    def _frame(ids, f):
+        import pandas as pd
+        return pd.DataFrame({"id": ids, "features": list(f)})
+
+    @property
+    def userFactors(self):
+        return self._frame(*self.user_factors_np())
+
+    @property
+    def itemFactors(self):
+        return self._frame(*self.item_factors_np())
+
+    # ---- ALSModel.transform ---------------------------------------------------------------------
+    def transform(self, dataset):
+        import pandas as pd
+        user = _checked_cast(_column(dataset, self._p["userCol"]), self._p["userCol"])
+        item = _checked_cast(_column(dataset, self._p["itemCol"]), self._p["itemCol"])
+        out = np.empty(user.size, dtype=np.float32)
+        check(load().als_predict(self._h, user.size, ptr(np.ascontiguousarray(user), C.c_int32),
+                                 ptr(np.ascontiguousarray(item), C.c_int32), ptr(out, C.c_float)))
+        df = pd.DataFrame(dataset).copy() if not isinstance(dataset, pd.DataFrame) else dataset.copy()
+        df[self._p["predictionCol"]] = out
+        if self._p["coldStartStrategy"] == "drop":
+            df = df[~np.isnan(out)]
+        return df
+
+    # ---- recommendForAll* / recommendFor*Subset ------------------------------------------------
+    def _recommend(self, side, num, subset=None):
+        lib = load()
+        if subset is not None:
+            sub = np.ascontiguousarray(np.unique(np.asarray(subset, dtype=np.int32)))
+            nq = sub.size
+        else:
+            sub = None
+            nq = lib.als_num_rows(self._h, side)
+        src = np.empty(nq, dtype=np.int32)
+        ids = np.empty((nq, num), dtype=np.int32)
+        sc = np.empty((nq, num), dtype=np.float32)
+        check(lib.als_recommend(self._h, side, int(num), ptr(sub, C.c_int32) if sub is not None else None,
+                                nq, ptr(src, C.c_int32), ptr(ids, C.c_int32), ptr(sc, C.c_float)))
+        return src, ids, sc
+
+    def recommend_np(self, num, subset=None, side=_lib.ALS_USER):
+        """(src ids, dst ids [n, num], scores [n, num]) sorted (score desc, id asc); -1/NaN padding."""
+        return self._recommend(side, num, subset)
+
+    def _rec_frame(self, src, ids, sc, src_col, dst_col):
+        import pandas as pd
+        recs = []
+        for r in range(len(src)):
+            m = ids[r] >= 0
+            recs.append([(int(i), float(s)) for i, s in zip(ids[r][m], sc[r][m])])
+        keep = [i for i in range(len(src)) if recs[i]]
+        return pd.DataFrame({src_col: src[keep], "recommendations": [recs[i] for i in keep]})
+
+    def recommendForAllUsers(self, numItems):
+        return self._rec_frame(*self._recommend(_lib.ALS_USER, numItems), self._p["userCol"], self._p["itemCol"])
+
+    def recommendForAllItems(self, numUsers):
+        return self._rec_frame(*self._recommend(_lib.ALS_ITEM, numUsers), self._p["itemCol"], self._p["userCol"])
+
+    def recommendForUserSubset(self, dataset, numItems):
+        users = _column(dataset, self._p["userCol"])
+        return self._rec_frame(*self._recommend(_lib.ALS_USER, numItems, users), self._p["userCol"],
+                               self._p["itemCol"])
+
+    def recommendForItemSubset(self, dataset, numUsers):
+        items = _column(dataset, self._p["itemCol"])
+        return self._rec_frame(*self._recommend(_lib.ALS_ITEM, numUsers, items), self._p["itemCol"],
+                               self._p["userCol"])
+
+    # ---- persistence (Spark ML layout: metadata/part-00000 + userFactors/ + itemFactors/ parquet) ---
+    def save(self, path, overwrite=False):
+        import shutil
+        import pyarrow as pa
+        import pyarrow.parquet as pq
+        if os.path.exists(path):
+            if not overwrite:
+                raise IOError(f"Path {path} already exists. To overwrite it, please use write.overwrite().save(path).")
+            shutil.rmtree(path)
+        os.makedirs(os.path.join(path, "metadata"))
+        meta = {"class": "org.apache.spark.ml.recommendation.ALSModel", "timestamp": int(time.time() * 1000),
+                "sparkVersion": "2.2.0", "uid": "als_albedo_mi355x",
+                "paramMap": {k: self._p[k] for k in ("userCol", "itemCol", "predictionCol", "coldStartStrategy")},
+                "rank": self.rank}
+        with open(os.path.join(path, "metadata", "part-00000"), "w") as fh:
+            fh.write(json.dumps(meta, separators=(",", ":")) + "\n")
+        open(os.path.join(path, "metadata", "_SUCCESS"), "w").close()
+        for name, (ids, f) in (("userFactors", self.user_factors_np()), ("itemFactors", self.item_factors_np())):
+            os.makedirs(os.path.join(path, name))
+            table = pa.table({"id": pa.array(ids, pa.int32()),
+                              "features": pa.array(list(f), pa.list_(pa.float32()))})
+            pq.write_table(table, os.path.join(path, name, "part-00000.parquet"))
+            open(os.path.join(path, name, "_SUCCESS"), "w").close()
+
+    def write(self):
+        model = self
+
+        class _Writer:
+            _ow = False
+
+            def overwrite(self):
+                self._ow = True
+                return self
+
+            def save(self, path):
+                model.save(path, overwrite=self._ow)
+
+        return _Writer()
+
+    @classmethod
+    def load(cls, path, device=-1):
+        import glob
+        import pyarrow.parquet as pq
+        with open(os.path.join(path, "metadata", "part-00000")) as fh:
+            meta = json.loads(fh.readline())
+        rank = int(meta["rank"])
+
+        def read(name):
+            parts = sorted(glob.glob(os.path.join(path, name, "*.parquet")))
+            ids, feats = [], []
+            for p in parts:
+                t = pq.read_table(p)
+                ids.append(np.asarray(t.column("id").to_numpy(), dtype=np.int32))
+                feats.append(np.asarray(t.column("features").to_pylist(), dtype=np.float32).reshape(-1, rank))
+            if not parts:
+                return np.empty(0, np.int32), np.empty((0, rank), np.float32)
+            return np.concatenate(ids), np.concatenate(feats)
+
+        uid, uf = read("userFactors")
+        iid, itf = read("itemFactors")
+        h = C.c_void_p()
+        check(load().als_model_create(rank, uid.size, ptr(uid, C.c_int32), ptr(uf, C.c_float), iid.size,
+                                      ptr(iid, C.c_int32), ptr(itf, C.c_float), int(device), C.byref(h)))
+        params = dict(_Params._defaults)
+        params.update(meta.get("paramMap", {}))
+        params["rank"] = rank
+        return cls(h, params)

@@ -1,0 +1,1051 @@
+// libalbedo_als.so host engine: the C ABI of include/albedo_als.h.
+//
+// Mirrors Spark MLlib 2.2.0 ALS.train as reached from ALSRecommenderBuilder.scala:46-58:
+//   userFactors = initialize(...); itemFactors = initialize(...)
+//   for iter in 1..maxIter: itemFactors = computeFactors(userFactors -> items)
+//                           userFactors = computeFactors(itemFactors -> users)
+// Each computeFactors call is one half-sweep here (half_sweep()):
+//   G = Σ y yᵀ over the src rows (MFMA, fp64 partials)    [+ all-reduce across ranks]
+//   G = P Λ Pᵀ (host fp64 eigensolver);  Z = X_src · P    [+ all-gather of the Z shard]
+//   every dst row solved in the eigenbasis (light: push-through, heavy: explicit Cholesky)
+// Factors are stored in a per-side basis B (original = X · Bᵀ); solving from src basis B_s with
+// rotation P puts the dst solution in basis B_s·P, so only one rotation GEMM runs per half-sweep.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "albedo_als.h"
+#include "host_math.h"
+#include "kernels.h"
+
+using namespace albedo;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                                  \
+  do {                                                                                             \
+    hipError_t e_ = (x);                                                                           \
+    if (e_ != hipSuccess)                                                                          \
+      return fail(e_ == hipErrorOutOfMemory ? ALS_E_OUT_OF_MEMORY : ALS_E_HIP,                     \
+                  std::string("HIP error: ") + hipGetErrorString(e_) + " in " #x);                 \
+  } while (0)
+#define NCCLCHK(x)                                                                                 \
+  do {                                                                                             \
+    ncclResult_t r_ = (x);                                                                         \
+    if (r_ != ncclSuccess) return fail(ALS_E_RCCL, std::string("RCCL error: ") + ncclGetErrorString(r_) + " in " #x); \
+  } while (0)
+#define TRYC(x)                    \
+  do {                             \
+    int rc_ = (x);                 \
+    if (rc_ != ALS_OK) return rc_; \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  hipError_t ensure(size_t b) {
+    if (b <= bytes && p) return hipSuccess;
+    release();
+    hipError_t e = hipMalloc(&p, b ? b : 16);
+    if (e == hipSuccess) bytes = b;
+    return e;
+  }
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+enum { B_L16 = 0, B_L32 = 1, B_L64 = 2, B_HEAVY = 3, NBUCKET = 4 };
+
+struct Side {
+  int64_t n = 0;                 // rows (unique raw ids)
+  std::vector<int32_t> ids;      // ascending
+  std::vector<int64_t> starts;   // shard starts over dense rows (world + 1)
+  int64_t maxrows = 0;           // rows per rank in the padded (gathered) layout
+  int64_t own0 = 0, own_n = 0;   // this rank's dense row range
+  // dst CSR of this side restricted to own rows (local row index; col = padded src position)
+  DevBuf d_ptr, d_col, d_val;
+  int64_t own_nnz = 0;
+  std::vector<int64_t> h_deg;    // degree per own row
+  DevBuf d_rows;                 // own local rows grouped by bucket
+  int64_t boff[NBUCKET + 1] = {0};
+  int64_t bnnz[NBUCKET] = {0};
+  DevBuf d_X;                    // [own_n][KP] factors in basis B
+  DevBuf d_Z;                    // [world*maxrows][KP] rotated factors (src role)
+  std::vector<double> B;         // [KP][KP] basis: original = X · Bᵀ
+  std::vector<double> G;         // last Gram of this side (as src), [rank][rank]
+  bool has_factors = false;
+  double t[ALS_T_COUNT] = {0};
+  int64_t stats[4] = {0};
+  DevBuf d_orig;                 // [n][KP] original-basis factors, dense order (materialised)
+  bool orig_valid = false;
+};
+
+}  // namespace
+
+struct als_ctx {
+  als_params p{};
+  int KP = 0;
+  int dev = 0;
+  hipStream_t st = nullptr;
+  int rank = 0, world = 1;
+  ncclComm_t comm = nullptr;
+  // host transport (tests: several processes sharing one GPU exchange through the host)
+  int (*h_allreduce)(void*, double*, int64_t) = nullptr;
+  int (*h_allgather)(void*, float*, int64_t) = nullptr;
+  void* h_user = nullptr;
+  Side s[2];
+  int64_t nnz = 0;
+  bool has_ratings = false;
+  bool model_only = false;
+  DevBuf slab, d_G, d_P, d_lam, d_err;
+  int slab_blocks = 0;
+  hipEvent_t ev[8] = {};
+};
+
+namespace {
+
+int set_device(als_ctx* c) {
+  HIPCHK(hipSetDevice(c->dev));
+  return ALS_OK;
+}
+
+int validate(const als_params* p) {
+  auto bad = [](const char* name, double v) {
+    char buf[160];
+    snprintf(buf, sizeof buf, "als parameter %s given invalid value %g.", name, v);
+    return fail(ALS_E_INVALID_ARGUMENT, buf);
+  };
+  if (p->rank < 1) return bad("rank", p->rank);
+  if (p->max_iter < 0) return bad("maxIter", p->max_iter);
+  if (!(p->reg_param >= 0)) return bad("regParam", p->reg_param);
+  if (!(p->alpha >= 0)) return bad("alpha", p->alpha);
+  if (p->num_user_blocks < 1) return bad("numUserBlocks", p->num_user_blocks);
+  if (p->num_item_blocks < 1) return bad("numItemBlocks", p->num_item_blocks);
+  if (padded_rank(p->rank) == 0)
+    return fail(ALS_E_UNSUPPORTED, "rank " + std::to_string(p->rank) + " exceeds the compiled maximum (128)");
+  return ALS_OK;
+}
+
+int64_t light_limit(const als_ctx* c) {
+  if (c->p.light_max_degree >= 0) return std::min<int64_t>(c->p.light_max_degree, 64);
+  return c->KP >= 128 ? 64 : 32;
+}
+
+int bucket_of(int64_t d, int64_t lmax) {
+  if (d <= lmax) {
+    if (d <= 16) return B_L16;
+    if (d <= 32) return B_L32;
+    return B_L64;
+  }
+  return B_HEAVY;
+}
+
+// ---- collectives ------------------------------------------------------------------------------
+int allreduce_G(als_ctx* c) {
+  const int64_t n = (int64_t)c->KP * c->KP;
+  if (c->world == 1) return ALS_OK;
+  if (c->comm) {
+    NCCLCHK(ncclAllReduce(c->d_G.p, c->d_G.p, n, ncclDouble, ncclSum, c->comm, c->st));
+    return ALS_OK;
+  }
+  std::vector<double> h(n);
+  HIPCHK(hipMemcpyAsync(h.data(), c->d_G.p, n * 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  if (c->h_allreduce(c->h_user, h.data(), n) != 0) return fail(ALS_E_RCCL, "host all-reduce callback failed");
+  HIPCHK(hipMemcpyAsync(c->d_G.p, h.data(), n * 8, hipMemcpyHostToDevice, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return ALS_OK;
+}
+
+int allgather_rows(als_ctx* c, float* buf, int64_t rows_per_rank) {
+  if (c->world == 1) return ALS_OK;
+  const int64_t per = rows_per_rank * c->KP;
+  if (c->comm) {
+    NCCLCHK(ncclAllGather(buf + (int64_t)c->rank * per, buf, per, ncclFloat, c->comm, c->st));
+    return ALS_OK;
+  }
+  std::vector<float> h((size_t)per * c->world);
+  HIPCHK(hipMemcpyAsync(h.data() + (size_t)c->rank * per, buf + (int64_t)c->rank * per, per * 4,
+                        hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  if (c->h_allgather(c->h_user, h.data(), per) != 0) return fail(ALS_E_RCCL, "host all-gather callback failed");
+  HIPCHK(hipMemcpyAsync(buf, h.data(), h.size() * 4, hipMemcpyHostToDevice, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return ALS_OK;
+}
+
+// padded position of dense row i of side S
+inline int64_t padded_pos(const Side& S, int64_t i) {
+  const auto it = std::upper_bound(S.starts.begin(), S.starts.end(), i);
+  const int64_t r = (int64_t)(it - S.starts.begin()) - 1;
+  return r * S.maxrows + (i - S.starts[r]);
+}
+
+// ---- ingest -------------------------------------------------------------------------------------
+int ingest_device(als_ctx* c, int64_t n, const int32_t* d_user, const int32_t* d_item, const float* d_rating) {
+  if (n <= 0)
+    return fail(ALS_E_INVALID_ARGUMENT, "No ratings available from the input dataset (empty ratings).");
+  TRYC(set_device(c));
+  hipStream_t st = c->st;
+  DevBuf ud, id;
+  HIPCHK(ud.ensure(n * 4));
+  HIPCHK(id.ensure(n * 4));
+  int32_t *uu = nullptr, *ii = nullptr;
+  int64_t nu = 0, ni = 0;
+  HIPCHK(remap_ids(d_user, n, ud.as<int32_t>(), &uu, &nu, st));
+  HIPCHK(remap_ids(d_item, n, id.as<int32_t>(), &ii, &ni, st));
+  Side& U = c->s[ALS_USER];
+  Side& I = c->s[ALS_ITEM];
+  U.n = nu;
+  I.n = ni;
+  U.ids.resize(nu);
+  I.ids.resize(ni);
+  HIPCHK(hipMemcpy(U.ids.data(), uu, nu * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(I.ids.data(), ii, ni * 4, hipMemcpyDeviceToHost));
+  (void)hipFree(uu);
+  (void)hipFree(ii);
+  c->nnz = n;
+  // both orientations, full, then sliced to this rank's rows
+  struct Full { DevBuf ptr, col, val; std::vector<int64_t> hptr; } full[2];
+  for (int side = 0; side < 2; ++side) {
+    Side& S = c->s[side];
+    Full& F = full[side];
+    HIPCHK(F.ptr.ensure((S.n + 1) * 8));
+    HIPCHK(F.col.ensure(n * 4));
+    HIPCHK(F.val.ensure(n * 4));
+    const int32_t* dst = side == ALS_USER ? ud.as<int32_t>() : id.as<int32_t>();
+    const int32_t* src = side == ALS_USER ? id.as<int32_t>() : ud.as<int32_t>();
+    HIPCHK(build_csr(dst, src, d_rating, n, S.n, c->s[1 - side].n, F.ptr.as<int64_t>(), F.col.as<int32_t>(),
+                     F.val.as<float>(), st));
+    F.hptr.resize(S.n + 1);
+    HIPCHK(hipMemcpy(F.hptr.data(), F.ptr.p, (S.n + 1) * 8, hipMemcpyDeviceToHost));
+    S.starts.assign(c->world + 1, 0);
+    plan_shards(F.hptr.data(), S.n, c->world, S.starts.data());
+    S.maxrows = 0;
+    for (int r = 0; r < c->world; ++r) S.maxrows = std::max<int64_t>(S.maxrows, S.starts[r + 1] - S.starts[r]);
+    S.own0 = S.starts[c->rank];
+    S.own_n = S.starts[c->rank + 1] - S.own0;
+  }
+  ud.release();
+  id.release();
+  const int64_t lmax = light_limit(c);
+  for (int side = 0; side < 2; ++side) {
+    Side& S = c->s[side];
+    Side& Src = c->s[1 - side];
+    Full& F = full[side];
+    const int64_t e0 = F.hptr[S.own0], e1 = F.hptr[S.own0 + S.own_n];
+    S.own_nnz = e1 - e0;
+    std::vector<int64_t> lp(S.own_n + 1);
+    for (int64_t r = 0; r <= S.own_n; ++r) lp[r] = F.hptr[S.own0 + r] - e0;
+    HIPCHK(S.d_ptr.ensure((S.own_n + 1) * 8));
+    HIPCHK(hipMemcpy(S.d_ptr.p, lp.data(), (S.own_n + 1) * 8, hipMemcpyHostToDevice));
+    HIPCHK(S.d_col.ensure(S.own_nnz * 4));
+    HIPCHK(S.d_val.ensure(S.own_nnz * 4));
+    HIPCHK(hipMemcpy(S.d_val.p, F.val.as<float>() + e0, S.own_nnz * 4, hipMemcpyDeviceToDevice));
+    if (c->world == 1) {
+      HIPCHK(hipMemcpy(S.d_col.p, F.col.as<int32_t>() + e0, S.own_nnz * 4, hipMemcpyDeviceToDevice));
+    } else {  // dense src index -> padded src position
+      std::vector<int32_t> hc(S.own_nnz);
+      HIPCHK(hipMemcpy(hc.data(), F.col.as<int32_t>() + e0, S.own_nnz * 4, hipMemcpyDeviceToHost));
+      for (auto& v : hc) v = (int32_t)padded_pos(Src, v);
+      HIPCHK(hipMemcpy(S.d_col.p, hc.data(), S.own_nnz * 4, hipMemcpyHostToDevice));
+    }
+    // degree buckets (heavy rows longest first for the tail)
+    S.h_deg.resize(S.own_n);
+    std::vector<int32_t> rows[NBUCKET];
+    for (int64_t r = 0; r < S.own_n; ++r) {
+      S.h_deg[r] = lp[r + 1] - lp[r];
+      const int b = bucket_of(S.h_deg[r], lmax);
+      rows[b].push_back((int32_t)r);
+      S.bnnz[b] += S.h_deg[r];
+    }
+    std::stable_sort(rows[B_HEAVY].begin(), rows[B_HEAVY].end(),
+                     [&](int32_t a, int32_t b) { return S.h_deg[a] > S.h_deg[b]; });
+    std::vector<int32_t> all;
+    all.reserve(S.own_n);
+    for (int b = 0; b < NBUCKET; ++b) {
+      S.boff[b] = (int64_t)all.size();
+      all.insert(all.end(), rows[b].begin(), rows[b].end());
+    }
+    S.boff[NBUCKET] = (int64_t)all.size();
+    HIPCHK(S.d_rows.ensure(all.size() * 4));
+    HIPCHK(hipMemcpy(S.d_rows.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
+  }
+  for (int side = 0; side < 2; ++side) {
+    Side& S = c->s[side];
+    HIPCHK(S.d_X.ensure((size_t)std::max<int64_t>(S.own_n, 1) * c->KP * 4));
+    HIPCHK(S.d_Z.ensure((size_t)std::max<int64_t>(c->world * S.maxrows, 1) * c->KP * 4));
+    HIPCHK(hipMemset(S.d_X.p, 0, S.d_X.bytes));
+    HIPCHK(hipMemset(S.d_Z.p, 0, S.d_Z.bytes));
+    S.B.assign((size_t)c->KP * c->KP, 0.0);
+    for (int i = 0; i < c->KP; ++i) S.B[(size_t)i * c->KP + i] = 1.0;
+    S.has_factors = false;
+    S.orig_valid = false;
+  }
+  const int64_t maxsrc = std::max(c->s[0].own_n, c->s[1].own_n);
+  c->slab_blocks = gram_slab_blocks(c->KP, maxsrc);
+  HIPCHK(c->slab.ensure(gram_slab_doubles(c->KP, c->slab_blocks) * 8));
+  HIPCHK(c->d_G.ensure((size_t)c->KP * c->KP * 8));
+  HIPCHK(c->d_P.ensure((size_t)c->KP * c->KP * 4));
+  HIPCHK(c->d_lam.ensure((size_t)c->KP * 4));
+  HIPCHK(c->d_err.ensure(16));
+  c->has_ratings = true;
+  return ALS_OK;
+}
+
+// upload host factors (dense order, [n][rank]) for this rank's own rows
+int upload_factors(als_ctx* c, int side, const float* f, int64_t ld) {
+  Side& S = c->s[side];
+  std::vector<float> h((size_t)std::max<int64_t>(S.own_n, 1) * c->KP, 0.f);
+  for (int64_t r = 0; r < S.own_n; ++r)
+    std::memcpy(&h[(size_t)r * c->KP], f + (size_t)(S.own0 + r) * ld, sizeof(float) * c->p.rank);
+  HIPCHK(hipMemcpy(S.d_X.p, h.data(), (size_t)S.own_n * c->KP * 4, hipMemcpyHostToDevice));
+  S.B.assign((size_t)c->KP * c->KP, 0.0);
+  for (int i = 0; i < c->KP; ++i) S.B[(size_t)i * c->KP + i] = 1.0;
+  S.has_factors = true;
+  S.orig_valid = false;
+  return ALS_OK;
+}
+
+int spark_init(als_ctx* c) {
+  int64_t su, si;
+  spark_side_seeds(c->p.seed, &su, &si);
+  for (int side = 0; side < 2; ++side) {
+    Side& S = c->s[side];
+    std::vector<float> f((size_t)S.n * c->p.rank);
+    spark_initialize(S.ids.data(), S.n, c->p.rank, side == ALS_USER ? su : si,
+                     side == ALS_USER ? c->p.num_user_blocks : c->p.num_item_blocks, f.data(), c->p.rank);
+    TRYC(upload_factors(c, side, f.data(), c->p.rank));
+  }
+  return ALS_OK;
+}
+
+float event_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, a, b);
+  return ms;
+}
+
+int half_sweep(als_ctx* c, int t) {
+  const int sidx = 1 - t;
+  Side& S = c->s[sidx];
+  Side& T = c->s[t];
+  if (!S.has_factors) return fail(ALS_E_STATE, "source factors are not initialised");
+  const int KP = c->KP, k = c->p.rank;
+  hipStream_t st = c->st;
+  hipEvent_t* ev = c->ev;
+  float* zown = S.d_Z.as<float>() + (size_t)c->rank * S.maxrows * KP;
+  double eig_ms = 0.0;
+  bool force_heavy = c->p.light_max_degree == 0;
+  HIPCHK(hipEventRecord(ev[0], st));
+  if (c->p.implicit_prefs) {
+    HIPCHK(launch_gram(KP, S.d_X.as<float>(), S.own_n, c->slab.as<double>(), c->slab_blocks, c->d_G.as<double>(), st));
+    TRYC(allreduce_G(c));
+    HIPCHK(hipEventRecord(ev[1], st));
+    std::vector<double> Gf((size_t)KP * KP);
+    HIPCHK(hipMemcpyAsync(Gf.data(), c->d_G.p, Gf.size() * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<double> Gk((size_t)k * k), w(k), V((size_t)k * k);
+    for (int i = 0; i < k; ++i)
+      for (int j = 0; j < k; ++j) Gk[(size_t)i * k + j] = Gf[(size_t)i * KP + j];
+    S.G = Gk;
+    if (!sym_eig(k, Gk.data(), w.data(), V.data()))
+      return fail(ALS_E_NOT_POSITIVE_DEFINITE, "eigendecomposition of the Gram matrix did not converge");
+    std::vector<float> P32((size_t)KP * KP, 0.f), lam32(KP, 0.f);
+    std::vector<double> Pf((size_t)KP * KP, 0.0);
+    for (int i = 0; i < KP; ++i) Pf[(size_t)i * KP + i] = 1.0;
+    for (int i = 0; i < k; ++i)
+      for (int j = 0; j < k; ++j) Pf[(size_t)i * KP + j] = V[(size_t)i * k + j];
+    for (size_t e = 0; e < Pf.size(); ++e) P32[e] = (float)Pf[e];
+    double wmax = 0.0, wmin = INFINITY;
+    for (int i = 0; i < k; ++i) {
+      lam32[i] = (float)std::max(w[i], 0.0);
+      wmax = std::max(wmax, w[i]);
+      wmin = std::min(wmin, w[i]);
+    }
+    if (!(wmin > 1e-12 * wmax) && c->p.reg_param == 0.0) force_heavy = true;
+    if (!(wmin > 1e-12 * wmax)) {
+      // the push-through form needs Λ + λn > 0 for every row; rows without positive ratings have n = 0
+      force_heavy = force_heavy || c->p.reg_param == 0.0;
+    }
+    // new basis of the dst side: B_t = B_s · P
+    std::vector<double> Bn((size_t)KP * KP, 0.0);
+    for (int i = 0; i < KP; ++i)
+      for (int m = 0; m < KP; ++m) {
+        const double b = S.B[(size_t)i * KP + m];
+        if (b == 0.0) continue;
+        const double* pr = &Pf[(size_t)m * KP];
+        double* out = &Bn[(size_t)i * KP];
+        for (int j = 0; j < KP; ++j) out[j] += b * pr[j];
+      }
+    T.B.swap(Bn);
+    eig_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    HIPCHK(hipMemcpyAsync(c->d_P.p, P32.data(), P32.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->d_lam.p, lam32.data(), lam32.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(ev[2], st));
+    HIPCHK(launch_rotate(KP, S.d_X.as<float>(), c->d_P.as<float>(), zown, S.own_n, st));
+  } else {
+    HIPCHK(hipEventRecord(ev[1], st));
+    HIPCHK(hipMemsetAsync(c->d_lam.p, 0, KP * 4, st));
+    T.B = S.B;
+    if (c->p.reg_param == 0.0) force_heavy = true;
+    HIPCHK(hipEventRecord(ev[2], st));
+    HIPCHK(hipMemcpyAsync(zown, S.d_X.p, (size_t)S.own_n * KP * 4, hipMemcpyDeviceToDevice, st));
+  }
+  HIPCHK(hipEventRecord(ev[3], st));
+  TRYC(allgather_rows(c, S.d_Z.as<float>(), S.maxrows));
+  HIPCHK(hipEventRecord(ev[4], st));
+  HIPCHK(hipMemsetAsync(c->d_err.p, 0, 4, st));
+  SolveArgs a{};
+  a.Z = S.d_Z.as<float>();
+  a.ptr = T.d_ptr.as<int64_t>();
+  a.col = T.d_col.as<int32_t>();
+  a.val = T.d_val.as<float>();
+  a.lam = c->d_lam.as<float>();
+  a.X = T.d_X.as<float>();
+  a.kreal = k;
+  a.implicit = c->p.implicit_prefs;
+  a.alpha = (float)c->p.alpha;
+  a.reg = (float)c->p.reg_param;
+  a.err = c->d_err.as<int>();
+  const int32_t* rows = T.d_rows.as<int32_t>();
+  static const int Dof[3] = {16, 32, 64};
+  T.stats[0] = T.stats[1] = T.stats[2] = T.stats[3] = 0;
+  for (int b = 0; b < 3; ++b) {
+    a.rows = rows + T.boff[b];
+    a.n_rows = T.boff[b + 1] - T.boff[b];
+    if (force_heavy) HIPCHK(launch_solve_heavy(KP, a, st));
+    else HIPCHK(launch_solve_light(KP, Dof[b], a, st));
+    T.stats[force_heavy ? 2 : 0] += a.n_rows;
+    T.stats[force_heavy ? 3 : 1] += T.bnnz[b];
+  }
+  HIPCHK(hipEventRecord(ev[5], st));
+  a.rows = rows + T.boff[B_HEAVY];
+  a.n_rows = T.boff[B_HEAVY + 1] - T.boff[B_HEAVY];
+  HIPCHK(launch_solve_heavy(KP, a, st));
+  T.stats[2] += a.n_rows;
+  T.stats[3] += T.bnnz[B_HEAVY];
+  HIPCHK(hipEventRecord(ev[6], st));
+  int err = 0;
+  HIPCHK(hipMemcpyAsync(&err, c->d_err.p, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  T.t[ALS_T_GRAM] = event_ms(ev[0], ev[1]);
+  T.t[ALS_T_EIG] = eig_ms;
+  T.t[ALS_T_ROTATE] = event_ms(ev[2], ev[3]);
+  T.t[ALS_T_COMM] = event_ms(ev[3], ev[4]);
+  T.t[ALS_T_SOLVE_LIGHT] = event_ms(ev[4], ev[5]);
+  T.t[ALS_T_SOLVE_HEAVY] = event_ms(ev[5], ev[6]);
+  T.t[ALS_T_HALF_TOTAL] = event_ms(ev[0], ev[6]);
+  if (err & 3)
+    return fail(ALS_E_NOT_POSITIVE_DEFINITE,
+                "LAPACK.dppsv-equivalent Cholesky met a non-positive pivot because A is not positive "
+                "definite. Is A derived from a singular matrix (e.g. collinear column values)?");
+  T.has_factors = true;
+  T.orig_valid = false;
+  return ALS_OK;
+}
+
+// original-basis factors of `side`, dense order, on device: d_orig [n][KP]
+int materialize(als_ctx* c, int side) {
+  Side& S = c->s[side];
+  if (S.orig_valid) return ALS_OK;
+  if (!S.has_factors) return fail(ALS_E_STATE, "factors are not available (call fit first)");
+  const int KP = c->KP;
+  std::vector<float> Bt((size_t)KP * KP);
+  for (int i = 0; i < KP; ++i)
+    for (int j = 0; j < KP; ++j) Bt[(size_t)i * KP + j] = (float)S.B[(size_t)j * KP + i];
+  HIPCHK(c->d_P.ensure((size_t)KP * KP * 4));
+  HIPCHK(hipMemcpyAsync(c->d_P.p, Bt.data(), Bt.size() * 4, hipMemcpyHostToDevice, c->st));
+  DevBuf padded;
+  const int64_t prows = c->world * S.maxrows;
+  HIPCHK(padded.ensure((size_t)std::max<int64_t>(prows, 1) * KP * 4));
+  float* own = padded.as<float>() + (size_t)c->rank * S.maxrows * KP;
+  HIPCHK(launch_rotate(KP, S.d_X.as<float>(), c->d_P.as<float>(), own, S.own_n, c->st));
+  TRYC(allgather_rows(c, padded.as<float>(), S.maxrows));
+  HIPCHK(S.d_orig.ensure((size_t)std::max<int64_t>(S.n, 1) * KP * 4));
+  for (int r = 0; r < c->world; ++r) {
+    const int64_t nr = S.starts[r + 1] - S.starts[r];
+    if (nr > 0)
+      HIPCHK(hipMemcpyAsync(S.d_orig.as<float>() + (size_t)S.starts[r] * KP,
+                            padded.as<float>() + (size_t)r * S.maxrows * KP, (size_t)nr * KP * 4,
+                            hipMemcpyDeviceToDevice, c->st));
+  }
+  HIPCHK(hipStreamSynchronize(c->st));
+  S.orig_valid = true;
+  return ALS_OK;
+}
+
+int64_t find_row(const Side& S, int32_t id) {
+  auto it = std::lower_bound(S.ids.begin(), S.ids.end(), id);
+  if (it == S.ids.end() || *it != id) return -1;
+  return it - S.ids.begin();
+}
+
+}  // namespace
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+extern "C" {
+
+const char* als_last_error(void) { return g_err.c_str(); }
+int als_abi_version(void) { return ALBEDO_ALS_ABI_VERSION; }
+
+int als_device_count(int* out) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  int good = 0;
+  for (int d = 0; d < n; ++d) {
+    hipDeviceProp_t pr;
+    if (hipGetDeviceProperties(&pr, d) == hipSuccess && std::strncmp(pr.gcnArchName, "gfx950", 6) == 0) ++good;
+  }
+  *out = good;
+  return ALS_OK;
+}
+
+int als_params_default(als_params* p) {
+  if (!p) return fail(ALS_E_INVALID_ARGUMENT, "null params");
+  p->rank = 10;
+  p->max_iter = 10;
+  p->implicit_prefs = 0;
+  p->nonnegative = 0;
+  p->num_user_blocks = 10;
+  p->num_item_blocks = 10;
+  p->reg_param = 0.1;
+  p->alpha = 1.0;
+  p->seed = 0;
+  p->device = -1;
+  p->light_max_degree = -1;
+  return ALS_OK;
+}
+
+static int ctx_common(const als_params* p, als_ctx** out) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(ALS_E_NO_DEVICE, "no HIP device visible: the ALS engine runs on MI355X (gfx950) only");
+  auto* c = new als_ctx();
+  c->p = *p;
+  c->KP = padded_rank(p->rank);
+  if (p->device >= 0) c->dev = p->device;
+  else if (hipGetDevice(&c->dev) != hipSuccess) c->dev = 0;
+  if (c->dev >= ndev) {
+    delete c;
+    return fail(ALS_E_NO_DEVICE, "device ordinal out of range");
+  }
+  hipDeviceProp_t pr;
+  if (hipGetDeviceProperties(&pr, c->dev) != hipSuccess || std::strncmp(pr.gcnArchName, "gfx950", 6) != 0) {
+    delete c;
+    return fail(ALS_E_NO_DEVICE, "device is not gfx950 (MI355X)");
+  }
+  if (hipSetDevice(c->dev) != hipSuccess || hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return fail(ALS_E_HIP, "failed to create a HIP stream");
+  }
+  for (auto& e : c->ev) (void)hipEventCreate(&e);
+  *out = c;
+  return ALS_OK;
+}
+
+int als_create(const als_params* p, als_ctx** out) {
+  if (!p || !out) return fail(ALS_E_INVALID_ARGUMENT, "null argument");
+  *out = nullptr;
+  TRYC(validate(p));
+  if (p->nonnegative)
+    return fail(ALS_E_UNSUPPORTED, "nonnegative=true (NNLS solver) is not built in this engine version yet");
+  return ctx_common(p, out);
+}
+
+void als_destroy(als_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->dev);
+  if (c->st) (void)hipStreamSynchronize(c->st);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->st) (void)hipStreamDestroy(c->st);
+  delete c;
+}
+
+int als_comm_unique_id(void* out128) {
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  ncclUniqueId id;
+  NCCLCHK(ncclGetUniqueId(&id));
+  std::memcpy(out128, &id, sizeof id);
+  return ALS_OK;
+}
+
+int als_comm_init(als_ctx* c, int32_t rank, int32_t world, const void* id128) {
+  if (!c || !id128 || world < 1 || rank < 0 || rank >= world) return fail(ALS_E_INVALID_ARGUMENT, "bad comm args");
+  if (c->has_ratings) return fail(ALS_E_STATE, "als_comm_init must precede als_set_ratings");
+  TRYC(set_device(c));
+  c->rank = rank;
+  c->world = world;
+  if (world > 1) {
+    ncclUniqueId id;
+    std::memcpy(&id, id128, sizeof id);
+    NCCLCHK(ncclCommInitRank(&c->comm, world, id, rank));
+  }
+  return ALS_OK;
+}
+
+int als_comm_init_host(als_ctx* c, int32_t rank, int32_t world, int (*allreduce)(void*, double*, int64_t),
+                       int (*allgather)(void*, float*, int64_t), void* user) {
+  if (!c || world < 1 || rank < 0 || rank >= world || !allreduce || !allgather)
+    return fail(ALS_E_INVALID_ARGUMENT, "bad comm args");
+  if (c->has_ratings) return fail(ALS_E_STATE, "als_comm_init_host must precede als_set_ratings");
+  c->rank = rank;
+  c->world = world;
+  c->h_allreduce = allreduce;
+  c->h_allgather = allgather;
+  c->h_user = user;
+  return ALS_OK;
+}
+
+int als_set_ratings(als_ctx* c, int64_t n, const int32_t* user, const int32_t* item, const float* rating) {
+  if (!c) return fail(ALS_E_INVALID_ARGUMENT, "null context");
+  if (n <= 0) return fail(ALS_E_INVALID_ARGUMENT, "No ratings available from the input dataset (empty ratings).");
+  if (!user || !item || !rating) return fail(ALS_E_INVALID_ARGUMENT, "null ratings");
+  TRYC(set_device(c));
+  DevBuf du, di, dr;
+  HIPCHK(du.ensure(n * 4));
+  HIPCHK(di.ensure(n * 4));
+  HIPCHK(dr.ensure(n * 4));
+  HIPCHK(hipMemcpy(du.p, user, n * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(di.p, item, n * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dr.p, rating, n * 4, hipMemcpyHostToDevice));
+  return ingest_device(c, n, du.as<int32_t>(), di.as<int32_t>(), dr.as<float>());
+}
+
+int als_set_ratings_device(als_ctx* c, int64_t n, const int32_t* du, const int32_t* di, const float* dr) {
+  if (!c) return fail(ALS_E_INVALID_ARGUMENT, "null context");
+  return ingest_device(c, n, du, di, dr);
+}
+
+int64_t als_num_rows(const als_ctx* c, int side) {
+  if (!c || (side != 0 && side != 1)) return -1;
+  return c->s[side].n;
+}
+int64_t als_num_ratings(const als_ctx* c) { return c ? c->nnz : -1; }
+int als_rank(const als_ctx* c) { return c ? c->p.rank : -1; }
+
+int als_get_ids(const als_ctx* c, int side, int32_t* out) {
+  if (!c || (side != 0 && side != 1) || !out) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  std::memcpy(out, c->s[side].ids.data(), c->s[side].ids.size() * 4);
+  return ALS_OK;
+}
+
+int als_set_initial_factors(als_ctx* c, int side, int64_t n, const int32_t* ids, const float* f) {
+  if (!c || (side != 0 && side != 1) || !ids || !f) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  if (!c->has_ratings) return fail(ALS_E_STATE, "set ratings before injecting factors");
+  TRYC(set_device(c));
+  Side& S = c->s[side];
+  const int k = c->p.rank;
+  std::vector<float> dense((size_t)S.n * k, 0.f);
+  std::vector<char> seen(S.n, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t r = find_row(S, ids[i]);
+    if (r < 0) continue;  // ids absent from the ratings are ignored, like Spark's join
+    std::memcpy(&dense[(size_t)r * k], f + (size_t)i * k, sizeof(float) * k);
+    seen[r] = 1;
+  }
+  for (int64_t r = 0; r < S.n; ++r)
+    if (!seen[r]) return fail(ALS_E_INVALID_ARGUMENT, "initial factors missing for id " + std::to_string(S.ids[r]));
+  return upload_factors(c, side, dense.data(), k);
+}
+
+int als_init_factors(als_ctx* c) {
+  if (!c) return fail(ALS_E_INVALID_ARGUMENT, "null context");
+  if (!c->has_ratings) return fail(ALS_E_STATE, "set ratings first");
+  TRYC(set_device(c));
+  return spark_init(c);
+}
+
+int als_init_factors_random(als_ctx* c, uint64_t seed) {
+  if (!c) return fail(ALS_E_INVALID_ARGUMENT, "null context");
+  if (!c->has_ratings) return fail(ALS_E_STATE, "set ratings first");
+  TRYC(set_device(c));
+  for (int side = 0; side < 2; ++side) {
+    Side& S = c->s[side];
+    HIPCHK(launch_init_random(c->KP, c->p.rank, S.d_X.as<float>(), S.own_n, seed + 0x51ED270B27u * (side + 1),
+                              S.own0, c->st));
+    S.B.assign((size_t)c->KP * c->KP, 0.0);
+    for (int i = 0; i < c->KP; ++i) S.B[(size_t)i * c->KP + i] = 1.0;
+    S.has_factors = true;
+    S.orig_valid = false;
+  }
+  HIPCHK(hipStreamSynchronize(c->st));
+  return ALS_OK;
+}
+
+int als_half_sweep(als_ctx* c, int dst_side) {
+  if (!c || (dst_side != 0 && dst_side != 1)) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  if (!c->has_ratings) return fail(ALS_E_STATE, "set ratings first");
+  TRYC(set_device(c));
+  return half_sweep(c, dst_side);
+}
+
+int als_run_sweeps(als_ctx* c, int32_t n) {
+  if (!c) return fail(ALS_E_INVALID_ARGUMENT, "null context");
+  if (!c->has_ratings) return fail(ALS_E_STATE, "set ratings first");
+  TRYC(set_device(c));
+  for (int it = 0; it < n; ++it) {
+    TRYC(half_sweep(c, ALS_ITEM));
+    TRYC(half_sweep(c, ALS_USER));
+  }
+  return ALS_OK;
+}
+
+int als_fit(als_ctx* c) {
+  if (!c) return fail(ALS_E_INVALID_ARGUMENT, "null context");
+  if (!c->has_ratings)
+    return fail(ALS_E_INVALID_ARGUMENT, "No ratings available from the input dataset (empty ratings).");
+  TRYC(set_device(c));
+  if (!c->s[0].has_factors || !c->s[1].has_factors) TRYC(spark_init(c));
+  return als_run_sweeps(c, c->p.max_iter);
+}
+
+int als_get_gram(als_ctx* c, int src_side, double* out) {
+  if (!c || (src_side != 0 && src_side != 1) || !out) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  const auto& G = c->s[src_side].G;
+  if (G.empty()) return fail(ALS_E_STATE, "no Gram computed yet");
+  std::memcpy(out, G.data(), G.size() * 8);
+  return ALS_OK;
+}
+
+int als_get_factors(als_ctx* c, int side, int32_t* ids_out, float* f_out) {
+  if (!c || (side != 0 && side != 1)) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  TRYC(set_device(c));
+  TRYC(materialize(c, side));
+  Side& S = c->s[side];
+  if (ids_out) std::memcpy(ids_out, S.ids.data(), S.n * 4);
+  if (f_out) {
+    const int KP = c->KP, k = c->p.rank;
+    std::vector<float> h((size_t)S.n * KP);
+    HIPCHK(hipMemcpy(h.data(), S.d_orig.p, h.size() * 4, hipMemcpyDeviceToHost));
+    for (int64_t r = 0; r < S.n; ++r) std::memcpy(f_out + (size_t)r * k, &h[(size_t)r * KP], sizeof(float) * k);
+  }
+  return ALS_OK;
+}
+
+int als_model_create(int32_t rank, int64_t nu, const int32_t* uids, const float* uf, int64_t ni,
+                     const int32_t* iids, const float* ifac, int32_t device, als_ctx** out) {
+  if (!out) return fail(ALS_E_INVALID_ARGUMENT, "null out");
+  *out = nullptr;
+  als_params p;
+  als_params_default(&p);
+  p.rank = rank;
+  p.device = device;
+  TRYC(validate(&p));
+  if (nu < 0 || ni < 0 || (nu && (!uids || !uf)) || (ni && (!iids || !ifac)))
+    return fail(ALS_E_INVALID_ARGUMENT, "bad factor arrays");
+  als_ctx* c = nullptr;
+  TRYC(ctx_common(&p, &c));
+  c->model_only = true;
+  const int64_t ns[2] = {nu, ni};
+  const int32_t* ids[2] = {uids, iids};
+  const float* fs[2] = {uf, ifac};
+  for (int side = 0; side < 2; ++side) {
+    Side& S = c->s[side];
+    std::vector<int64_t> ord(ns[side]);
+    std::iota(ord.begin(), ord.end(), 0);
+    std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return ids[side][a] < ids[side][b]; });
+    S.n = ns[side];
+    S.ids.resize(S.n);
+    std::vector<float> h((size_t)std::max<int64_t>(S.n, 1) * c->KP, 0.f);
+    for (int64_t r = 0; r < S.n; ++r) {
+      S.ids[r] = ids[side][ord[r]];
+      if (r > 0 && S.ids[r] == S.ids[r - 1]) {
+        als_destroy(c);
+        return fail(ALS_E_INVALID_ARGUMENT, "duplicate id in factors");
+      }
+      std::memcpy(&h[(size_t)r * c->KP], fs[side] + (size_t)ord[r] * rank, sizeof(float) * rank);
+    }
+    if (S.d_orig.ensure(h.size() * 4) != hipSuccess ||
+        hipMemcpy(S.d_orig.p, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+      als_destroy(c);
+      return fail(ALS_E_OUT_OF_MEMORY, "failed to upload factors");
+    }
+    S.orig_valid = true;
+    S.has_factors = true;
+    S.starts = {0, S.n};
+    S.maxrows = S.n;
+  }
+  *out = c;
+  return ALS_OK;
+}
+
+int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_t n_subset, int32_t* src_ids_out,
+                  int32_t* dst_ids_out, float* scores_out) {
+  if (!c || (side != 0 && side != 1) || !dst_ids_out || !scores_out)
+    return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  if (k <= 0) return fail(ALS_E_INVALID_ARGUMENT, "num must be positive");
+  if (k > TOPK_KC) return fail(ALS_E_UNSUPPORTED, "top-k above 64 is not supported by this engine version");
+  TRYC(set_device(c));
+  const int src = side, dst = 1 - side;
+  TRYC(materialize(c, src));
+  TRYC(materialize(c, dst));
+  Side& S = c->s[src];
+  Side& T = c->s[dst];
+  const int KP = c->KP;
+  const int64_t nq = subset ? n_subset : S.n;
+  std::vector<int32_t> qrow(nq);
+  for (int64_t i = 0; i < nq; ++i) qrow[i] = subset ? (int32_t)find_row(S, subset[i]) : (int32_t)i;
+  if (src_ids_out)
+    for (int64_t i = 0; i < nq; ++i) src_ids_out[i] = subset ? subset[i] : S.ids[i];
+  for (int64_t i = 0; i < nq * k; ++i) {
+    dst_ids_out[i] = -1;
+    scores_out[i] = NAN;
+  }
+  std::vector<int32_t> known;
+  std::vector<int64_t> pos;
+  for (int64_t i = 0; i < nq; ++i)
+    if (qrow[i] >= 0) {
+      known.push_back(qrow[i]);
+      pos.push_back(i);
+    }
+  if (known.empty() || T.n == 0) return ALS_OK;
+  // max dst row norm (error bound of the MFMA pre-selection)
+  double tmax = 0.0;
+  {
+    std::vector<float> h((size_t)T.n * KP);
+    HIPCHK(hipMemcpy(h.data(), T.d_orig.p, h.size() * 4, hipMemcpyDeviceToHost));
+    for (int64_t r = 0; r < T.n; ++r) {
+      double s2 = 0.0;
+      for (int j = 0; j < c->p.rank; ++j) s2 += (double)h[(size_t)r * KP + j] * h[(size_t)r * KP + j];
+      tmax = std::max(tmax, std::sqrt(s2));
+    }
+  }
+  DevBuf d_dstids;
+  HIPCHK(d_dstids.ensure(T.n * 4));
+  HIPCHK(hipMemcpy(d_dstids.p, T.ids.data(), T.n * 4, hipMemcpyHostToDevice));
+  const int64_t chunk = 1 << 20;
+  DevBuf d_src, d_cand, d_cs, d_oid, d_osc, d_need, d_flag;
+  for (int64_t q0 = 0; q0 < (int64_t)known.size(); q0 += chunk) {
+    const int64_t nc = std::min<int64_t>(chunk, (int64_t)known.size() - q0);
+    HIPCHK(d_src.ensure(nc * 4));
+    HIPCHK(d_cand.ensure(nc * TOPK_KC * 4));
+    HIPCHK(d_cs.ensure(nc * TOPK_KC * 4));
+    HIPCHK(d_oid.ensure(nc * k * 4));
+    HIPCHK(d_osc.ensure(nc * k * 4));
+    HIPCHK(d_need.ensure(nc * 4));
+    HIPCHK(hipMemcpy(d_src.p, known.data() + q0, nc * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(d_need.p, 0, nc * 4));
+    TopkArgs a{};
+    a.S = S.d_orig.as<float>();
+    a.T = T.d_orig.as<float>();
+    a.src_rows = d_src.as<int32_t>();
+    a.n_src = nc;
+    a.n_dst = T.n;
+    a.dst_ids = d_dstids.as<int32_t>();
+    a.kreal = c->p.rank;
+    a.k = k;
+    a.tmax_norm = (float)(tmax * (1.0 + 1e-6));
+    a.cand = d_cand.as<int32_t>();
+    a.cand_score = d_cs.as<float>();
+    a.out_ids = d_oid.as<int32_t>();
+    a.out_scores = d_osc.as<float>();
+    a.need_exact = d_need.as<int32_t>();
+    HIPCHK(launch_topk(KP, a, c->st));
+    std::vector<int32_t> need(nc);
+    HIPCHK(hipMemcpyAsync(need.data(), d_need.p, nc * 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    std::vector<int32_t> flagged;
+    for (int64_t i = 0; i < nc; ++i)
+      if (need[i]) flagged.push_back((int32_t)i);
+    if (!flagged.empty()) {
+      HIPCHK(d_flag.ensure(flagged.size() * 4));
+      HIPCHK(hipMemcpy(d_flag.p, flagged.data(), flagged.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(launch_topk_exact(KP, a, d_flag.as<int32_t>(), (int64_t)flagged.size(), c->st));
+    }
+    std::vector<int32_t> oid(nc * k);
+    std::vector<float> osc(nc * k);
+    HIPCHK(hipMemcpyAsync(oid.data(), d_oid.p, oid.size() * 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(osc.data(), d_osc.p, osc.size() * 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    for (int64_t i = 0; i < nc; ++i) {
+      std::memcpy(dst_ids_out + pos[q0 + i] * k, &oid[i * k], k * 4);
+      std::memcpy(scores_out + pos[q0 + i] * k, &osc[i * k], k * 4);
+    }
+  }
+  return ALS_OK;
+}
+
+int als_predict(als_ctx* c, int64_t n, const int32_t* user, const int32_t* item, float* out) {
+  if (!c || (n > 0 && (!user || !item || !out))) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  if (n <= 0) return ALS_OK;
+  TRYC(set_device(c));
+  TRYC(materialize(c, ALS_USER));
+  TRYC(materialize(c, ALS_ITEM));
+  std::vector<int32_t> u(n), v(n);
+  for (int64_t i = 0; i < n; ++i) {
+    u[i] = (int32_t)find_row(c->s[ALS_USER], user[i]);
+    v[i] = (int32_t)find_row(c->s[ALS_ITEM], item[i]);
+  }
+  DevBuf du, dv, dout;
+  HIPCHK(du.ensure(n * 4));
+  HIPCHK(dv.ensure(n * 4));
+  HIPCHK(dout.ensure(n * 4));
+  HIPCHK(hipMemcpy(du.p, u.data(), n * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dv.p, v.data(), n * 4, hipMemcpyHostToDevice));
+  HIPCHK(launch_predict(c->KP, c->p.rank, c->s[ALS_USER].d_orig.as<float>(), c->s[ALS_ITEM].d_orig.as<float>(),
+                        du.as<int32_t>(), dv.as<int32_t>(), dout.as<float>(), n, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  HIPCHK(hipMemcpy(out, dout.p, n * 4, hipMemcpyDeviceToHost));
+  return ALS_OK;
+}
+
+int als_get_row_ratings(als_ctx* c, int side, int32_t id, int64_t cap, int32_t* src_ids, float* ratings,
+                        int64_t* n_out) {
+  if (!c || (side != 0 && side != 1) || !n_out) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  if (!c->has_ratings) return fail(ALS_E_STATE, "set ratings first");
+  TRYC(set_device(c));
+  Side& S = c->s[side];
+  const Side& Src = c->s[1 - side];
+  const int64_t r = find_row(S, id);
+  if (r < 0) return fail(ALS_E_INVALID_ARGUMENT, "unknown id " + std::to_string(id));
+  if (r < S.own0 || r >= S.own0 + S.own_n) return fail(ALS_E_STATE, "row not owned by this rank");
+  int64_t pr[2];
+  HIPCHK(hipMemcpy(pr, S.d_ptr.as<int64_t>() + (r - S.own0), 16, hipMemcpyDeviceToHost));
+  const int64_t n = pr[1] - pr[0];
+  *n_out = n;
+  if (n > cap) return ALS_OK;
+  std::vector<int32_t> col(n);
+  if (n) {
+    HIPCHK(hipMemcpy(col.data(), S.d_col.as<int32_t>() + pr[0], n * 4, hipMemcpyDeviceToHost));
+    if (ratings) HIPCHK(hipMemcpy(ratings, S.d_val.as<float>() + pr[0], n * 4, hipMemcpyDeviceToHost));
+  }
+  if (src_ids)
+    for (int64_t e = 0; e < n; ++e) {
+      const int64_t p = col[e];
+      const int64_t rk = Src.maxrows ? p / Src.maxrows : 0;
+      src_ids[e] = Src.ids[Src.starts[rk] + (p - rk * Src.maxrows)];
+    }
+  return ALS_OK;
+}
+
+int als_last_timings(const als_ctx* c, int dst_side, double* out, int n) {
+  if (!c || (dst_side != 0 && dst_side != 1) || !out) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  for (int i = 0; i < n && i < ALS_T_COUNT; ++i) out[i] = c->s[dst_side].t[i];
+  return ALS_OK;
+}
+
+int als_path_stats(const als_ctx* c, int dst_side, int64_t* out4) {
+  if (!c || (dst_side != 0 && dst_side != 1) || !out4) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  for (int i = 0; i < 4; ++i) out4[i] = c->s[dst_side].stats[i];
+  return ALS_OK;
+}
+
+int als_synchronize(als_ctx* c) {
+  if (!c) return fail(ALS_E_INVALID_ARGUMENT, "null context");
+  TRYC(set_device(c));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return ALS_OK;
+}
+
+int als_synth_generate(int32_t device, uint64_t seed, int32_t rounds, int64_t n_users, int64_t n_items,
+                       const int64_t* deg_prefix, const double* cw, const int32_t* perm, int32_t* user_out,
+                       int32_t* item_out, float* rating_out, int64_t* n_out) {
+  if (!deg_prefix || !cw || !perm || !n_out || n_users <= 0 || n_items <= 0)
+    return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(ALS_E_NO_DEVICE, "no HIP device");
+  if (device >= 0) HIPCHK(hipSetDevice(device));
+  const int64_t n = deg_prefix[n_users];
+  DevBuf dp, dcw, dperm, du, di, dr;
+  HIPCHK(dp.ensure((n_users + 1) * 8));
+  HIPCHK(dcw.ensure(n_items * 8));
+  HIPCHK(dperm.ensure(n_items * 4));
+  HIPCHK(du.ensure(n * 4));
+  HIPCHK(di.ensure(n * 4));
+  HIPCHK(dr.ensure(n * 4));
+  HIPCHK(hipMemcpy(dp.p, deg_prefix, (n_users + 1) * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dcw.p, cw, n_items * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dperm.p, perm, n_items * 4, hipMemcpyHostToDevice));
+  hipStream_t st;
+  HIPCHK(hipStreamCreate(&st));
+  hipError_t e = synth_fill(seed, rounds, n_users, n_items, dp.as<int64_t>(), dcw.as<double>(), dperm.as<int32_t>(),
+                            du.as<int32_t>(), di.as<int32_t>(), dr.as<float>(), n, n_out, st);
+  (void)hipStreamDestroy(st);
+  HIPCHK(e);
+  if (user_out) HIPCHK(hipMemcpy(user_out, du.p, *n_out * 4, hipMemcpyDeviceToHost));
+  if (item_out) HIPCHK(hipMemcpy(item_out, di.p, *n_out * 4, hipMemcpyDeviceToHost));
+  if (rating_out) HIPCHK(hipMemcpy(rating_out, dr.p, *n_out * 4, hipMemcpyDeviceToHost));
+  return ALS_OK;
+}
+
+int als_set_ratings_synthetic(als_ctx* c, uint64_t seed, int32_t rounds, int64_t n_users, int64_t n_items,
+                              const int64_t* deg_prefix, const double* cw, const int32_t* perm) {
+  if (!c || !deg_prefix || !cw || !perm || n_users <= 0 || n_items <= 0)
+    return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  TRYC(set_device(c));
+  const int64_t n = deg_prefix[n_users];
+  DevBuf dp, dcw, dperm, du, di, dr;
+  HIPCHK(dp.ensure((n_users + 1) * 8));
+  HIPCHK(dcw.ensure(n_items * 8));
+  HIPCHK(dperm.ensure(n_items * 4));
+  HIPCHK(du.ensure(n * 4));
+  HIPCHK(di.ensure(n * 4));
+  HIPCHK(dr.ensure(n * 4));
+  HIPCHK(hipMemcpy(dp.p, deg_prefix, (n_users + 1) * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dcw.p, cw, n_items * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dperm.p, perm, n_items * 4, hipMemcpyHostToDevice));
+  int64_t nout = 0;
+  HIPCHK(synth_fill(seed, rounds, n_users, n_items, dp.as<int64_t>(), dcw.as<double>(), dperm.as<int32_t>(),
+                    du.as<int32_t>(), di.as<int32_t>(), dr.as<float>(), n, &nout, c->st));
+  dp.release();
+  dcw.release();
+  dperm.release();
+  return ingest_device(c, nout, du.as<int32_t>(), di.as<int32_t>(), dr.as<float>());
+}
+
+// ---- host-only utilities (no GPU needed; used by the CPU test suite) ------------------------
+int als_host_eigh(int32_t n, const double* a, double* w, double* v) {
+  if (n <= 0 || !a || !w || !v) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  if (!sym_eig(n, a, w, v)) return fail(ALS_E_NOT_POSITIVE_DEFINITE, "eigensolver did not converge");
+  return ALS_OK;
+}
+
+int als_host_spark_side_seeds(int64_t seed, int64_t* user_seed, int64_t* item_seed) {
+  if (!user_seed || !item_seed) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  spark_side_seeds(seed, user_seed, item_seed);
+  return ALS_OK;
+}
+
+int als_host_spark_init(const int32_t* ids_sorted, int64_t n, int32_t rank, int64_t side_seed, int32_t num_blocks,
+                        float* out) {
+  if ((n > 0 && (!ids_sorted || !out)) || rank < 1 || num_blocks < 1) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  spark_initialize(ids_sorted, n, rank, side_seed, num_blocks, out, rank);
+  return ALS_OK;
+}
+
+int als_host_plan_shards(const int64_t* ptr, int64_t n, int32_t world, int64_t* starts_out) {
+  if (!ptr || n < 0 || world < 1 || !starts_out) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  plan_shards(ptr, n, world, starts_out);
+  return ALS_OK;
+}
+
+}  // extern "C"

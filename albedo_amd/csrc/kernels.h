@@ -1,0 +1,82 @@
+// Internal launch interface between the host engine (als_engine.cpp) and the HIP kernels.
+// Not part of the public C ABI (include/albedo_als.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace albedo {
+
+// Padded rank used on device: factor rows are KP floats (zero beyond `rank`).
+int padded_rank(int rank);  // 64 or 128 (0 if unsupported)
+
+struct SolveArgs {
+  const float* Z;          // src factors in the eigenbasis of the src Gram, [*][KP]
+  const int64_t* ptr;      // dst CSR row pointer (global dst row index)
+  const int32_t* col;      // src row index (into Z)
+  const float* val;        // rating
+  const int32_t* rows;     // dst rows handled by this launch
+  int64_t n_rows;
+  const float* lam;        // [KP] eigenvalues of the src Gram (implicit) or zeros (explicit)
+  float* X;                // out: dst factors in that eigenbasis, [*][KP]
+  int kreal;               // the model rank (<= KP)
+  int implicit;
+  float alpha;
+  float reg;
+  int* err;                // device flag: set to 1 when a solve meets a non-positive pivot
+};
+
+// G (fp64 [KP][KP], full symmetric) = Σ_rows Xᵀ X over rows [0, n) of X ([n][KP]).
+hipError_t launch_gram(int KP, const float* X, int64_t n, double* slab, int slab_blocks, double* G,
+                       hipStream_t s);
+int gram_slab_blocks(int KP, int64_t n);
+size_t gram_slab_doubles(int KP, int slab_blocks);
+
+// Z = X · M for n rows ([n][KP] · [KP][KP], row-major M).
+hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64_t n, hipStream_t s);
+
+// Per-row solves. light: rows with degree <= D (D in {16,32,64}); heavy: any degree.
+hipError_t launch_solve_light(int KP, int D, const SolveArgs& a, hipStream_t s);
+hipError_t launch_solve_heavy(int KP, const SolveArgs& a, hipStream_t s);
+
+// Seeded unit-norm Gaussian rows (global row index row0 + r) for large synthetic runs.
+hipError_t launch_init_random(int KP, int kreal, float* X, int64_t n, uint64_t seed, int64_t row0, hipStream_t s);
+
+// ALSModel.transform: out[p] = F2J sdot(U[u[p]], V[v[p]]) (NaN when u[p] < 0 or v[p] < 0).
+hipError_t launch_predict(int KP, int kreal, const float* U, const float* V, const int32_t* u,
+                          const int32_t* v, float* out, int64_t n, hipStream_t s);
+
+// Top-k: approximate (fp32 MFMA) top-KC candidates per src row, then exact F2J rescoring.
+struct TopkArgs {
+  const float* S;          // src factors (original basis) [*][KP]
+  const float* T;          // dst factors (original basis) [n_dst][KP]
+  const int32_t* src_rows; // src rows to score
+  int64_t n_src;
+  int64_t n_dst;
+  const int32_t* dst_ids;  // raw ids of dst rows (ascending with the row index)
+  int kreal;
+  int k;                   // requested top-k (<= 64)
+  float tmax_norm;         // max_j ||T_j||_2 (for the error bound)
+  int32_t* cand;           // [n_src][KC] scratch
+  float* cand_score;       // [n_src][KC] scratch
+  int32_t* out_ids;        // [n_src][k] raw dst ids
+  float* out_scores;       // [n_src][k]
+  int32_t* need_exact;     // [n_src] set when the candidate set could not be certified
+};
+hipError_t launch_topk(int KP, const TopkArgs& a, hipStream_t s);
+hipError_t launch_topk_exact(int KP, const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s);
+constexpr int TOPK_KC = 64;  // candidates kept per src row by the MFMA pass
+
+// Ingest (ingest.hip): COO -> remap + CSR.
+struct DeviceBuf;
+hipError_t remap_ids(const int32_t* d_ids, int64_t n, int32_t* d_dense, int32_t** d_unique,
+                     int64_t* n_unique, hipStream_t s);
+hipError_t build_csr(const int32_t* d_dst, const int32_t* d_src, const float* d_val, int64_t n,
+                     int64_t n_dst, int64_t n_src, int64_t* d_ptr, int32_t* d_col, float* d_valout,
+                     hipStream_t s);
+// Synthetic generator (synth.hip)
+hipError_t synth_fill(uint64_t seed, int rounds, int64_t n_users, int64_t n_items,
+                      const int64_t* d_deg_prefix, const double* d_cw, const int32_t* d_perm,
+                      int32_t* d_user, int32_t* d_item, float* d_rating, int64_t n_slots,
+                      int64_t* n_out, hipStream_t s);
+
+}  // namespace albedo

@@ -1,0 +1,248 @@
+"""Benchmark: implicit-ALS interactions/sec per sweep (BASELINE.json metric) on MI355X.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+A step = one full ALS sweep (item half-sweep + user half-sweep: Gram, eigendecomposition,
+rotation, RCCL all-reduce/all-gather, light + heavy per-row solves) over the whole synthetic star
+matrix, inputs resident in HBM.  Default workload = BASELINE config 4 (20M users x 4M repos,
+1B stars, rank 128: the config the metric is quoted on; it fits one 288 GB MI355X) row-sharded
+across ranks (strong scaling: the total work is fixed).  Rank 0 prints ONE JSON line.
+
+roofline: the dominant per-row solve kernel's algorithmic bytes per launch (SURVEY.md §8(d):
+  nnz·(4 col + 4 val) + (rows+1)·8 + nnz·4k gathered rows + rows·4k written) / its average
+  HIP-event duration on the engine's stream, against 8 TB/s HBM.
+cpu_baseline: the fp64 C/OpenMP restatement of Spark's half-sweep (oracle/c, "port") timed on a
+  bounded row sample of the same workload on this host, extrapolated to one sweep.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIG_RANK = {"c2": 64, "c4": 128, "c1p": 50}
+METRIC = "implicit-ALS interactions/sec per sweep at rank 128 (1/8 GPU); top-30 recs users/sec"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIG_RANK))
+    ap.add_argument("--topk-users", type=int, default=16384)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--light", type=int, default=-1)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch  # noqa: F401  (import before the engine: one HIP runtime per process)
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method="env://")
+    from albedo_amd import _lib as L
+    from albedo_amd.synthetic import CONFIGS, popularity_table, user_degrees
+
+    lib = L.load()
+    spec = CONFIGS[args.config]
+    k = CONFIG_RANK[args.config]
+    p = L.als_params()
+    L.check(lib.als_params_default(C.byref(p)))
+    p.rank, p.implicit_prefs, p.reg_param, p.alpha, p.seed = k, 1, 0.5, 40.0, 42
+    p.device = local
+    p.light_max_degree = args.light
+    h = C.c_void_p()
+    L.check(lib.als_create(C.byref(p), C.byref(h)))
+    if world > 1:
+        uid = (C.c_char * 128)()
+        if rank == 0:
+            L.check(lib.als_comm_unique_id(uid))
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=0)
+        uid = (C.c_char * 128).from_buffer_copy(obj[0])
+        L.check(lib.als_comm_init(h, rank, world, uid))
+
+    t0 = time.perf_counter()
+    deg = user_degrees(spec)
+    prefix = np.ascontiguousarray(np.r_[0, np.cumsum(deg)].astype(np.int64))
+    cw, perm = popularity_table(spec)
+    L.check(lib.als_set_ratings_synthetic(h, spec.seed, spec.rounds, spec.n_users, spec.n_items,
+                                          L.ptr(prefix, C.c_int64), L.ptr(np.ascontiguousarray(cw), C.c_double),
+                                          L.ptr(np.ascontiguousarray(perm), C.c_int32)))
+    L.check(lib.als_init_factors_random(h, 42))
+    setup_s = time.perf_counter() - t0
+    nnz = lib.als_num_ratings(h)
+    n_users, n_items = lib.als_num_rows(h, 0), lib.als_num_rows(h, 1)
+
+    def barrier():
+        L.check(lib.als_synchronize(h))
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        L.check(lib.als_run_sweeps(h, 1))
+    # per-stage device times accumulated over the timed sweeps
+    stage = {side: np.zeros(L.ALS_T_COUNT) for side in (0, 1)}
+    stats = {side: np.zeros(4, np.int64) for side in (0, 1)}
+    barrier()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        L.check(lib.als_half_sweep(h, 1))
+        tt = np.zeros(L.ALS_T_COUNT)
+        L.check(lib.als_last_timings(h, 1, L.ptr(tt, C.c_double), L.ALS_T_COUNT))
+        stage[1] += tt
+        L.check(lib.als_half_sweep(h, 0))
+        L.check(lib.als_last_timings(h, 0, L.ptr(tt, C.c_double), L.ALS_T_COUNT))
+        stage[0] += tt
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    for side in (0, 1):
+        L.check(lib.als_path_stats(h, side, L.ptr(stats[side], C.c_int64)))
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = nnz * args.steps / elapsed
+
+    # ---- roofline of the dominant solve kernel (per launch, this rank's shard) -------------------
+    def solve_bytes(side, which):  # which: 0 light, 1 heavy
+        rows, nz = stats[side][2 * which], stats[side][2 * which + 1]
+        return nz * 8 + (rows + 1) * 8 + nz * 4 * k + rows * 4 * k, rows, nz
+
+    kern = {}
+    for which, (name, ti, launches) in enumerate((("solve_light", L.T_NAMES.index("solve_light"), 3),
+                                                  ("solve_heavy", L.T_NAMES.index("solve_heavy"), 1))):
+        tot_ms = stage[0][ti] + stage[1][ti]
+        b = solve_bytes(0, which)[0] + solve_bytes(1, which)[0]
+        kern[name] = dict(ms=tot_ms / args.steps, bytes_per_sweep=b)
+    dom = max(kern, key=lambda n: kern[n]["ms"])
+    d = kern[dom]
+    achieved = d["bytes_per_sweep"] / (d["ms"] / 1000.0) / 1e9 if d["ms"] > 0 else 0.0
+    peak = 8000.0
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json")
+    if os.path.exists(tpath):
+        try:
+            traffic = json.load(open(tpath)).get(dom)
+        except Exception:
+            traffic = None
+
+    # ---- top-30 users/s (secondary metric; a bounded user subset) ------------------------------
+    topk_ups = None
+    if args.topk_users > 0 and world == 1:
+        ids = np.empty(n_users, np.int32)
+        L.check(lib.als_get_ids(h, 0, L.ptr(ids, C.c_int32)))
+        sub = np.ascontiguousarray(ids[np.linspace(0, n_users - 1, min(args.topk_users, n_users)).astype(np.int64)])
+        out_i = np.empty((sub.size, 30), np.int32)
+        out_s = np.empty((sub.size, 30), np.float32)
+        L.check(lib.als_recommend(h, 0, 30, L.ptr(sub[:1024], C.c_int32), min(1024, sub.size), None,
+                                  L.ptr(out_i, C.c_int32), L.ptr(out_s, C.c_float)))  # warm
+        t1 = time.perf_counter()
+        L.check(lib.als_recommend(h, 0, 30, L.ptr(sub, C.c_int32), sub.size, None, L.ptr(out_i, C.c_int32),
+                                  L.ptr(out_s, C.c_float)))
+        topk_ups = sub.size / (time.perf_counter() - t1)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(lib, L, h, k, nnz, n_users, n_items, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "interactions/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (seeded power-law star matrix, rating=1.0; SURVEY.md §8(d))",
+            "config": {"workload": f"BASELINE {args.config}: {n_users} users x {n_items} repos, {nnz} stars, "
+                                   f"rank {k}, implicit alpha 40 regParam 0.5, one sweep = item + user half",
+                       "rank": k, "nnz": int(nnz), "parallelism": f"row-shard x{world} (RCCL)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+                         "frac": achieved / peak, "traffic": traffic, "kernel": dom,
+                         "kernel_ms_per_sweep": d["ms"]},
+            "cpu_baseline": cpu,
+            "topk30_users_per_s": topk_ups,
+            "stages_ms_per_sweep": {f"{'user' if s == 0 else 'item'}_{n}": round((stage[s][i] / args.steps), 3)
+                                    for s in (0, 1) for i, n in enumerate(L.T_NAMES[:7])},
+            "paths": {"user": stats[0].tolist(), "item": stats[1].tolist()},
+            "setup_s": setup_s,
+        }
+        print(json.dumps(line), flush=True)
+    lib.als_destroy(h)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(lib, L, h, k, nnz, n_users, n_items, budget_s):
+    """fp64 C/OpenMP restatement (oracle/c) on a bounded sample of this workload's rows."""
+    from oracle import cbind
+    threads = min(16, os.cpu_count() or 1)
+    res = {}
+    for dst, n_dst, n_src in ((0, n_users, n_items), (1, n_items, n_users)):
+        src = 1 - dst
+        sids = np.empty(n_src, np.int32)
+        sf = np.empty((n_src, k), np.float32)
+        L.check(lib.als_get_factors(h, src, L.ptr(sids, C.c_int32), L.ptr(sf, C.c_float)))
+        t0 = time.perf_counter()
+        G = cbind.gram(sf, threads=threads)
+        g_s = time.perf_counter() - t0
+        dids = np.empty(n_dst, np.int32)
+        L.check(lib.als_get_ids(h, dst, L.ptr(dids, C.c_int32)))
+        rng = np.random.default_rng(7 + dst)
+        order = rng.permutation(n_dst)
+        ptr, cols, vals = [0], [], []
+        n_row = np.empty(1, np.int64)
+        total = 0
+        t_rows = 0.0
+        done = 0
+        chunk = 256
+        while done < n_dst and t_rows < budget_s / 2:
+            sel = order[done:done + chunk]
+            done += len(sel)
+            ptr, cols, vals = [0], [], []
+            for r in sel:
+                cap = 1 << 22
+                buf_i = np.empty(cap, np.int32)
+                buf_v = np.empty(cap, np.float32)
+                L.check(lib.als_get_row_ratings(h, dst, int(dids[r]), cap, L.ptr(buf_i, C.c_int32),
+                                                L.ptr(buf_v, C.c_float), L.ptr(n_row, C.c_int64)))
+                m = int(n_row[0])
+                cols.append(np.searchsorted(sids, buf_i[:m]).astype(np.int32))
+                vals.append(buf_v[:m].copy())
+                ptr.append(ptr[-1] + m)
+            ptr_a = np.asarray(ptr, np.int64)
+            t1 = time.perf_counter()
+            cbind.solve_rows(sf, G, ptr_a, np.concatenate(cols), np.concatenate(vals), reg=0.5, alpha=40.0,
+                             implicit=True, threads=threads)
+            t_rows += time.perf_counter() - t1
+            total += int(ptr_a[-1])
+            chunk = min(chunk * 2, 8192)
+        res[dst] = dict(gram_s=g_s, rows_s=t_rows, sample_nnz=total, sample_rows=done)
+        del sf
+    # extrapolate one sweep: Gram of each src side + per-nnz row cost over all stars
+    t_sweep = sum(res[d]["gram_s"] + res[d]["rows_s"] * (nnz / max(res[d]["sample_nnz"], 1)) for d in res)
+    return {"value": nnz / t_sweep, "unit": "interactions/s", "cores": threads, "kind": "port",
+            "sample": (f"fp64 C/OpenMP restatement of Spark's half-sweep (oracle/c/als_cpu.c): full Gram of each src "
+                       f"side + {res[0]['sample_rows']} user rows ({res[0]['sample_nnz']} stars) and "
+                       f"{res[1]['sample_rows']} repo rows ({res[1]['sample_nnz']} stars) solved, extrapolated "
+                       f"per star to one full sweep")}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,76 @@
+"""ctypes binding of oracle/c/liboracle_als.so — TEST INFRASTRUCTURE / CPU BASELINE ONLY."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "liboracle_als.so")
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        _lib = C.CDLL(_PATH)
+        P = C.c_void_p
+        _lib.oracle_half_sweep.restype = C.c_int
+        _lib.oracle_half_sweep.argtypes = [C.c_int64, P, P, P, C.c_int64, P, C.c_int, C.c_int, C.c_double,
+                                           C.c_double, P, C.c_int64, P, C.c_int]
+        _lib.oracle_solve_rows.restype = C.c_int
+        _lib.oracle_solve_rows.argtypes = [C.c_int64, P, P, P, P, C.c_int, C.c_int, C.c_double, C.c_double, P, P,
+                                           C.c_int64, P, C.c_int]
+        _lib.oracle_gram.restype = C.c_int
+        _lib.oracle_gram.argtypes = [C.c_int64, C.c_int, P, P, C.c_int]
+        _lib.oracle_max_threads.restype = C.c_int
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def half_sweep(Ysrc, ptr, col, val, *, reg, alpha, implicit=True, rows=None, threads=None):
+    lib = load()
+    Ysrc = np.ascontiguousarray(Ysrc, dtype=np.float32)
+    ptr = np.ascontiguousarray(ptr, dtype=np.int64)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    val = np.ascontiguousarray(val, dtype=np.float32)
+    n_dst = len(ptr) - 1
+    k = Ysrc.shape[1]
+    X = np.zeros((n_dst, k), dtype=np.float32)
+    rws = None if rows is None else np.ascontiguousarray(rows, dtype=np.int32)
+    nt = threads or lib.oracle_max_threads()
+    rc = lib.oracle_half_sweep(n_dst, _p(ptr), _p(col), _p(val), Ysrc.shape[0], _p(Ysrc), k, int(implicit),
+                               float(alpha), float(reg), _p(rws), 0 if rws is None else len(rws), _p(X), nt)
+    if rc != 0:
+        raise ValueError(f"oracle half-sweep: row {rc - 1} not positive definite (rc={rc})")
+    return X
+
+
+def gram(Y, threads=None):
+    lib = load()
+    Y = np.ascontiguousarray(Y, dtype=np.float32)
+    k = Y.shape[1]
+    G = np.zeros((k, k), dtype=np.float64)
+    lib.oracle_gram(Y.shape[0], k, _p(Y), _p(G), threads or lib.oracle_max_threads())
+    return G
+
+
+def solve_rows(Ysrc, G, ptr, col, val, *, reg, alpha, implicit=True, threads=None):
+    """Solve every row of the given CSR against src factors Ysrc with a precomputed Gram G."""
+    lib = load()
+    Ysrc = np.ascontiguousarray(Ysrc, dtype=np.float32)
+    G = np.ascontiguousarray(G, dtype=np.float64)
+    ptr = np.ascontiguousarray(ptr, dtype=np.int64)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    val = np.ascontiguousarray(val, dtype=np.float32)
+    n_dst = len(ptr) - 1
+    k = Ysrc.shape[1]
+    X = np.zeros((n_dst, k), dtype=np.float32)
+    rc = lib.oracle_solve_rows(n_dst, _p(ptr), _p(col), _p(val), _p(Ysrc), k, int(implicit), float(alpha),
+                               float(reg), _p(G), None, 0, _p(X), threads or lib.oracle_max_threads())
+    if rc != 0:
+        raise ValueError(f"oracle solve_rows: row {rc - 1} not positive definite (rc={rc})")
+    return X

@@ -1,0 +1,405 @@
+"""GPU parity: the HIP path through the C ABI against the CPU oracle and the golden fixtures.
+
+Tolerances (stated per SURVEY.md §8(c)):
+  * one half-sweep from identical inputs: max_row |x_gpu - x_oracle|_inf / |x_oracle|_inf <= 1e-4
+    (fp32 build + fp32 solve vs Spark's fp64; measured on trained factors at ~2e-5 worst);
+  * after a multi-sweep fit: factors within 1e-3 relative, RMSE within 1e-3 relative, NDCG@k
+    within 1e-3;
+  * top-k: ids and F2J scores bit-exact after the (score desc, id asc) tie-break;
+  * transform: bit-exact F2J sdot.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from oracle import spark_als as O
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _g(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+def _row_rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    num = np.max(np.abs(a - b), axis=1)
+    den = np.maximum(np.max(np.abs(b), axis=1), 1e-30)
+    return float(np.max(num / den))
+
+
+class Ctx:
+    """Thin test helper around the raw C ABI (parity tests call through the C ABI)."""
+
+    def __init__(self, lib, rank, implicit=True, reg=0.5, alpha=40.0, light=-1, max_iter=1):
+        from albedo_amd import _lib as L
+        self.L, self.lib = L, lib
+        p = L.als_params()
+        L.check(lib.als_params_default(C.byref(p)))
+        p.rank, p.implicit_prefs, p.reg_param, p.alpha = rank, int(implicit), reg, alpha
+        p.light_max_degree, p.max_iter = light, max_iter
+        self.h = C.c_void_p()
+        L.check(lib.als_create(C.byref(p), C.byref(self.h)))
+        self.rank = rank
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.als_destroy(self.h)
+
+    def ratings(self, user, item, rating):
+        L = self.L
+        u = np.ascontiguousarray(user, np.int32)
+        i = np.ascontiguousarray(item, np.int32)
+        r = np.ascontiguousarray(rating, np.float32)
+        L.check(self.lib.als_set_ratings(self.h, u.size, L.ptr(u, C.c_int32), L.ptr(i, C.c_int32),
+                                         L.ptr(r, C.c_float)))
+
+    def inject(self, side, ids, f):
+        L = self.L
+        ids = np.ascontiguousarray(ids, np.int32)
+        f = np.ascontiguousarray(f, np.float32)
+        L.check(self.lib.als_set_initial_factors(self.h, side, ids.size, L.ptr(ids, C.c_int32), L.ptr(f, C.c_float)))
+
+    def factors(self, side):
+        L = self.L
+        n = self.lib.als_num_rows(self.h, side)
+        ids = np.empty(n, np.int32)
+        f = np.empty((n, self.rank), np.float32)
+        L.check(self.lib.als_get_factors(self.h, side, L.ptr(ids, C.c_int32), L.ptr(f, C.c_float)))
+        return ids, f
+
+    def half(self, side):
+        self.L.check(self.lib.als_half_sweep(self.h, side))
+
+    def stats(self, side):
+        out = np.zeros(4, np.int64)
+        self.L.check(self.lib.als_path_stats(self.h, side, self.L.ptr(out, C.c_int64)))
+        return out
+
+
+# ---- ingest + Gram ---------------------------------------------------------------------------
+
+def test_ingest_remap_matches_oracle(gpu_lib):
+    f = _g("f1_half_sweep.npz")
+    B = O.make_blocks(f["user"], f["item"], f["rating"])
+    c = Ctx(gpu_lib, 8)
+    rng = np.random.default_rng(0)
+    perm = rng.permutation(f["user"].size)  # arbitrary input order
+    c.ratings(f["user"][perm], f["item"][perm], f["rating"][perm])
+    assert gpu_lib.als_num_rows(c.h, 0) == len(B.user_ids)
+    assert gpu_lib.als_num_rows(c.h, 1) == len(B.item_ids)
+    ids = np.empty(len(B.user_ids), np.int32)
+    c.L.check(gpu_lib.als_get_ids(c.h, 0, c.L.ptr(ids, C.c_int32)))
+    assert np.array_equal(ids, B.user_ids)
+
+
+@pytest.mark.parametrize("k", [8, 16])
+def test_golden_f1_half_sweep_and_gram(gpu_lib, k):
+    f = _g("f1_half_sweep.npz")
+    B = O.make_blocks(f["user"], f["item"], f["rating"])
+    for light in (-1, 0):  # engine default (push-through for light rows) and all-explicit
+        c = Ctx(gpu_lib, k, light=light)
+        c.ratings(f["user"], f["item"], f["rating"])
+        c.inject(0, B.user_ids, f[f"U0_k{k}"])
+        c.inject(1, B.item_ids, np.zeros((len(B.item_ids), k), np.float32))
+        c.half(1)
+        ids, V = c.factors(1)
+        assert np.array_equal(ids, B.item_ids)
+        assert _row_rel(V, f[f"V_k{k}"]) < 1e-4
+        G = np.empty((k, k))
+        c.L.check(gpu_lib.als_get_gram(c.h, 0, c.L.ptr(G, C.c_double)))
+        assert _rel(G, f[f"G_k{k}"]) < 1e-6
+        st = c.stats(1)
+        assert st[0] + st[2] == len(B.item_ids)
+        if light == 0:
+            assert st[0] == 0
+
+
+@pytest.mark.parametrize("k,light", [(50, -1), (50, 0), (64, -1), (100, -1), (128, 0), (128, -1)])
+def test_half_sweep_ranks_and_paths(gpu_lib, k, light):
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(1500, 600, 30000, seed=20 + k))
+    B = O.make_blocks(d["user"], d["item"], d["rating"])
+    rng = np.random.default_rng(k)
+    U0 = rng.standard_normal((len(B.user_ids), k)).astype(np.float32)
+    U0 /= np.linalg.norm(U0, axis=1, keepdims=True)
+    c = Ctx(gpu_lib, k, light=light)
+    c.ratings(d["user"], d["item"], d["rating"])
+    c.inject(0, B.user_ids, U0)
+    c.inject(1, B.item_ids, np.zeros((len(B.item_ids), k), np.float32))
+    c.half(1)
+    V_ref = O.half_sweep(U0, B.i_ptr, B.i_col, B.i_val, reg=0.5, alpha=40.0)
+    _, V = c.factors(1)
+    assert _row_rel(V, V_ref) < 1e-4
+    c.half(0)  # and back: user half-sweep from the GPU's item factors (exercises the basis chain)
+    U_ref = O.half_sweep(V, B.u_ptr, B.u_col, B.u_val, reg=0.5, alpha=40.0)
+    _, U = c.factors(0)
+    assert _row_rel(U, U_ref) < 1e-4
+
+
+def test_golden_f2_three_sweeps_fit(gpu_lib):
+    f = _g("f2_three_sweeps.npz")
+    B = O.make_blocks(f["user"], f["item"], f["rating"])
+    c = Ctx(gpu_lib, 16, max_iter=3)
+    c.ratings(f["user"], f["item"], f["rating"])
+    c.inject(0, B.user_ids, f["U0"])
+    c.inject(1, B.item_ids, f["V0"])
+    c.L.check(gpu_lib.als_fit(c.h))
+    _, U = c.factors(0)
+    _, V = c.factors(1)
+    assert _rel(U, f["U"]) < 1e-3 and _rel(V, f["V"]) < 1e-3
+    # RMSE of the implicit preference on observed pairs
+    def rmse(Uf, Vf):
+        p = O.f2j_sdot(Uf[B.u_ptr.searchsorted(np.arange(B.u_col.size), side="right") - 1], Vf[B.u_col])
+        return float(np.sqrt(np.mean((p - 1.0) ** 2)))
+    assert abs(rmse(U, V) - rmse(f["U"], f["V"])) <= 1e-3 * rmse(f["U"], f["V"])
+
+
+def test_golden_f3_explicit(gpu_lib):
+    f = _g("f3_explicit.npz")
+    B = O.make_blocks(f["user"], f["item"], f["rating"])
+    c = Ctx(gpu_lib, 10, implicit=False, reg=0.1, alpha=1.0, max_iter=2)
+    c.ratings(f["user"], f["item"], f["rating"])
+    c.inject(0, B.user_ids, f["U0"])
+    c.inject(1, B.item_ids, f["V0"])
+    c.L.check(gpu_lib.als_fit(c.h))
+    assert _rel(c.factors(0)[1], f["U"]) < 1e-3 and _rel(c.factors(1)[1], f["V"]) < 1e-3
+
+
+@pytest.mark.parametrize("light", [-1, 0])
+def test_golden_f6_zero_and_negative_ratings(gpu_lib, light):
+    f = _g("f6_zero_negative.npz")
+    B = O.make_blocks(f["user"], f["item"], f["rating"])
+    c = Ctx(gpu_lib, 8, light=light)
+    c.ratings(f["user"], f["item"], f["rating"])
+    c.inject(1, B.item_ids, f["V0"])
+    c.inject(0, B.user_ids, np.zeros((len(B.user_ids), 8), np.float32))
+    c.half(0)
+    assert _row_rel(c.factors(0)[1], f["U"]) < 1e-4
+
+
+def test_golden_f7_heavy_row(gpu_lib):
+    f = _g("f7_heavy_row.npz")
+    B = O.make_blocks(f["user"], f["item"], f["rating"])
+    assert np.max(np.diff(B.u_ptr)) >= 10000
+    c = Ctx(gpu_lib, 16)
+    c.ratings(f["user"], f["item"], f["rating"])
+    c.inject(1, B.item_ids, f["V0"])
+    c.inject(0, B.user_ids, np.zeros((len(B.user_ids), 16), np.float32))
+    c.half(0)
+    assert _row_rel(c.factors(0)[1], f["U"]) < 1e-4
+
+
+def test_not_positive_definite_raises(gpu_lib):
+    from albedo_amd import IllegalArgumentException
+    # explicit, regParam 0, every item rated by one user only: A = y yᵀ is singular for rank 4
+    user = np.array([1, 1, 2, 2], np.int32)
+    item = np.array([10, 11, 10, 11], np.int32)
+    c = Ctx(gpu_lib, 4, implicit=False, reg=0.0, alpha=1.0)
+    c.ratings(user, item, np.ones(4, np.float32))
+    c.inject(0, [1, 2], np.ones((2, 4), np.float32))
+    c.inject(1, [10, 11], np.ones((2, 4), np.float32))
+    with pytest.raises(IllegalArgumentException, match="not positive definite"):
+        c.half(1)
+
+
+# ---- Spark-style init, fit through the facade -----------------------------------------------
+
+def test_spark_init_on_device_matches_oracle(gpu_lib):
+    from albedo_amd import ALS
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(300, 100, 2000, seed=31))
+    B = O.make_blocks(d["user"], d["item"], d["rating"])
+    model = ALS(rank=7, maxIter=0, implicitPrefs=True, seed=42).fit(d)
+    su, si = O.spark_side_seeds(42)
+    assert np.array_equal(model.user_factors_np()[1], O.spark_initialize(B.user_ids, 7, su))
+    assert np.array_equal(model.item_factors_np()[1], O.spark_initialize(B.item_ids, 7, si))
+
+
+def test_facade_fit_matches_oracle_and_ndcg(gpu_lib):
+    from albedo_amd import ALS
+    from albedo_amd import evaluation as E
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(1200, 300, 14000, seed=32), with_timestamps=True)
+    B = O.make_blocks(d["user"], d["item"], d["rating"])
+    su, si = O.spark_side_seeds(42)
+    U0 = O.spark_initialize(B.user_ids, 12, su)
+    V0 = O.spark_initialize(B.item_ids, 12, si)
+    U, V = O.fit(B, rank=12, max_iter=4, reg=0.5, alpha=40.0, init_user=U0, init_item=V0)
+    als = (ALS().setImplicitPrefs(True).setRank(12).setRegParam(0.5).setAlpha(40).setMaxIter(4).setSeed(42)
+           .setColdStartStrategy("drop").setUserCol("user_id").setItemCol("repo_id").setRatingCol("starring"))
+    model = als.fit({"user_id": d["user"], "repo_id": d["item"], "starring": d["rating"]})
+    assert _rel(model.user_factors_np()[1], U) < 1e-3
+    assert _rel(model.item_factors_np()[1], V) < 1e-3
+    # albedo protocol: actual = 30 latest stars, predicted = top-30 by score
+    actual = E.into_user_items(d["user"], d["item"], d["ts"], 30)
+    sample = B.user_ids[::5]
+    src, ids, sc = model.recommend_np(30, subset=sample)
+    pred_gpu = {int(u): [int(x) for x in ids[r] if x >= 0] for r, u in enumerate(src)}
+    oid, _ = O.recommend_for_all(sample, U[np.searchsorted(B.user_ids, sample)], B.item_ids, V, 30)
+    pred_ref = {int(u): [int(x) for x in oid[r] if x >= 0] for r, u in enumerate(sample)}
+    n_gpu = E.RankingEvaluator(actual, "NDCG@k", 30).evaluate(pred_gpu)
+    n_ref = O.evaluate_ndcg(pred_ref, actual, 30)
+    assert abs(n_gpu - n_ref) <= 1e-3
+
+
+# ---- top-k and transform ---------------------------------------------------------------------
+
+@pytest.mark.parametrize("num", [30, 60])
+def test_golden_f4_topk_bit_exact_with_ties(gpu_lib, num):
+    from albedo_amd import _lib as L
+    f = _g("f4_topk_ties.npz")
+    h = C.c_void_p()
+    uid, uf = np.ascontiguousarray(f["uid"]), np.ascontiguousarray(f["uf"])
+    iid, itf = np.ascontiguousarray(f["iid"]), np.ascontiguousarray(f["itf"])
+    L.check(gpu_lib.als_model_create(12, uid.size, L.ptr(uid, C.c_int32), L.ptr(uf, C.c_float), iid.size,
+                                     L.ptr(iid, C.c_int32), L.ptr(itf, C.c_float), -1, C.byref(h)))
+    try:
+        nq = uid.size
+        src = np.empty(nq, np.int32)
+        ids = np.empty((nq, num), np.int32)
+        sc = np.empty((nq, num), np.float32)
+        L.check(gpu_lib.als_recommend(h, 0, num, None, nq, L.ptr(src, C.c_int32), L.ptr(ids, C.c_int32),
+                                      L.ptr(sc, C.c_float)))
+        order = np.argsort(uid)
+        assert np.array_equal(src, uid[order])
+        assert np.array_equal(ids, f[f"ids{num}"][order])
+        assert np.array_equal(sc.view(np.uint32), f[f"sc{num}"][order].view(np.uint32))
+    finally:
+        gpu_lib.als_destroy(h)
+
+
+def test_topk_subset_unknown_ids_and_small_catalogue(gpu_lib):
+    from albedo_amd import _lib as L
+    rng = np.random.default_rng(7)
+    uid = np.arange(50, dtype=np.int32) * 3
+    iid = np.arange(20, dtype=np.int32) * 5 - 40  # fewer items than k
+    uf = rng.standard_normal((50, 9)).astype(np.float32)
+    itf = rng.standard_normal((20, 9)).astype(np.float32)
+    h = C.c_void_p()
+    L.check(gpu_lib.als_model_create(9, 50, L.ptr(uid, C.c_int32), L.ptr(uf, C.c_float), 20, L.ptr(iid, C.c_int32),
+                                     L.ptr(itf, C.c_float), -1, C.byref(h)))
+    try:
+        sub = np.array([3, 4, 147], np.int32)  # 4 is unknown
+        ids = np.empty((3, 30), np.int32)
+        sc = np.empty((3, 30), np.float32)
+        L.check(gpu_lib.als_recommend(h, 0, 30, L.ptr(sub, C.c_int32), 3, None, L.ptr(ids, C.c_int32),
+                                      L.ptr(sc, C.c_float)))
+        ref, rs = O.recommend_for_all(np.array([3, 147]), uf[[1, 49]], iid, itf, 30)
+        assert np.array_equal(ids[[0, 2]], ref)
+        assert np.all(ids[1] == -1) and np.all(np.isnan(sc[1]))
+        assert np.all(ids[0, 20:] == -1)
+    finally:
+        gpu_lib.als_destroy(h)
+
+
+def test_transform_bit_exact_and_cold_start(gpu_lib):
+    from albedo_amd import ALS
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(400, 150, 4000, seed=33))
+    model = ALS(rank=11, maxIter=2, implicitPrefs=True, regParam=0.5, alpha=40.0,
+                coldStartStrategy="drop").fit(d)
+    uids, uf = model.user_factors_np()
+    iids, itf = model.item_factors_np()
+    q = {"user": np.r_[d["user"][:500], np.int32(-999)], "item": np.r_[d["item"][:500], d["item"][0]]}
+    out = model.transform(q)
+    assert len(out) == 500  # the unknown user is dropped
+    ref = O.f2j_sdot(uf[np.searchsorted(uids, q["user"][:500])], itf[np.searchsorted(iids, q["item"][:500])])
+    assert np.array_equal(out["prediction"].to_numpy().view(np.uint32), ref.view(np.uint32))
+    model.setColdStartStrategy("nan")
+    out2 = model.transform(q)
+    assert len(out2) == 501 and np.isnan(out2["prediction"].to_numpy()[-1])
+
+
+def test_model_save_load_roundtrip(gpu_lib, tmp_path):
+    from albedo_amd import ALS, ALSModel
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(300, 120, 3000, seed=34))
+    model = ALS(rank=6, maxIter=2, implicitPrefs=True).fit(d)
+    path = str(tmp_path / "alsModel.parquet")
+    model.write().overwrite().save(path)
+    m2 = ALSModel.load(path)
+    assert m2.rank == 6
+    assert np.array_equal(m2.user_factors_np()[1], model.user_factors_np()[1])
+    a = model.recommend_np(10)
+    b = m2.recommend_np(10)
+    assert all(np.array_equal(x, y, equal_nan=True) for x, y in zip(a, b))
+
+
+# ---- generator twin, scale properties ---------------------------------------------------------
+
+def test_device_synthetic_generator_matches_numpy(gpu_lib):
+    from albedo_amd import _lib as L
+    from albedo_amd.synthetic import SynthSpec, generate, popularity_table, user_degrees
+    spec = SynthSpec(3000, 500, 60000, seed=35)
+    ref = generate(spec)
+    deg = user_degrees(spec)
+    prefix = np.ascontiguousarray(np.r_[0, np.cumsum(deg)].astype(np.int64))
+    cw, perm = popularity_table(spec)
+    cw = np.ascontiguousarray(cw)
+    perm = np.ascontiguousarray(perm)
+    n = int(prefix[-1])
+    u = np.empty(n, np.int32)
+    i = np.empty(n, np.int32)
+    r = np.empty(n, np.float32)
+    nout = C.c_int64()
+    L.check(gpu_lib.als_synth_generate(-1, spec.seed, spec.rounds, spec.n_users, spec.n_items,
+                                       L.ptr(prefix, C.c_int64), L.ptr(cw, C.c_double), L.ptr(perm, C.c_int32),
+                                       L.ptr(u, C.c_int32), L.ptr(i, C.c_int32), L.ptr(r, C.c_float), C.byref(nout)))
+    m = nout.value
+    assert m == ref["user"].size
+    assert np.array_equal(u[:m], ref["user"]) and np.array_equal(i[:m], ref["item"])
+
+
+def test_c2_scale_rows_match_fp64_solve(gpu_lib):
+    """Full-size property at BASELINE config 2 (1M x 200k, 50M nnz, rank 64): after an item and a
+    user half-sweep from Spark-style init, sampled rows of every degree bucket equal the fp64
+    solution of Spark's normal equation built on the host from the engine's own inputs."""
+    from albedo_amd import _lib as L
+    from albedo_amd.synthetic import CONFIGS, popularity_table, user_degrees
+    spec = CONFIGS["c2"]
+    c = Ctx(gpu_lib, 64)
+    deg = user_degrees(spec)
+    prefix = np.ascontiguousarray(np.r_[0, np.cumsum(deg)].astype(np.int64))
+    cw, perm = popularity_table(spec)
+    L.check(gpu_lib.als_set_ratings_synthetic(c.h, spec.seed, spec.rounds, spec.n_users, spec.n_items,
+                                              L.ptr(prefix, C.c_int64), L.ptr(np.ascontiguousarray(cw), C.c_double),
+                                              L.ptr(np.ascontiguousarray(perm), C.c_int32)))
+    assert gpu_lib.als_num_ratings(c.h) > 0.99 * spec.nnz
+    L.check(gpu_lib.als_init_factors(c.h))
+    c.half(1)
+    c.half(0)
+    st = c.stats(0)
+    assert st[0] > 0 and st[2] > 0  # both solve paths ran
+    uids, U = c.factors(0)
+    iids, V = c.factors(1)
+    V64 = V.astype(np.float64)
+    G = V64.T @ V64
+    rng = np.random.default_rng(0)
+    n_row = np.empty(1, np.int64)
+    checked = 0
+    for r in rng.choice(len(uids), 200, replace=False):
+        cap = 50000
+        src = np.empty(cap, np.int32)
+        rat = np.empty(cap, np.float32)
+        L.check(gpu_lib.als_get_row_ratings(c.h, 0, int(uids[r]), cap, L.ptr(src, C.c_int32), L.ptr(rat, C.c_float),
+                                            L.ptr(n_row, C.c_int64)))
+        n = int(n_row[0])
+        Y = V64[np.searchsorted(iids, src[:n])]
+        cvec = 40.0 * np.abs(rat[:n].astype(np.float64))
+        A = G + (Y.T * cvec) @ Y + 0.5 * np.sum(rat[:n] > 0) * np.eye(64)
+        b = Y.T @ np.where(rat[:n] > 0, 1.0 + cvec, 0.0)
+        x = np.linalg.solve(A, b)
+        assert np.max(np.abs(U[r] - x)) / np.max(np.abs(x)) < 1e-4
+        checked += 1
+    assert checked == 200

@@ -1,0 +1,118 @@
+"""Host-side engine logic that needs no GPU: the C ABI library loads and exports every symbol the
+public header declares; eigensolver, Spark-style init, shard planning, parameter validation."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from tests.conftest import ROOT
+
+
+def _lib():
+    from albedo_amd import _lib
+    return _lib, _lib.load()
+
+
+def test_library_exports_every_header_symbol():
+    _, lib = _lib()
+    hdr = open(os.path.join(ROOT, "include", "albedo_als.h")).read()
+    names = set(re.findall(r"\b(als_[a-z0-9_]+)\s*\(", hdr))
+    assert len(names) > 25
+    for n in sorted(names):
+        assert hasattr(lib, n), f"libalbedo_als.so does not export {n}"
+    from albedo_amd import _lib as L
+    bound = {s[0] for s in L.SIGNATURES}
+    assert names == bound, f"header/binding mismatch: {names ^ bound}"
+
+
+def test_abi_version_and_error_string():
+    L, lib = _lib()
+    assert lib.als_abi_version() == 1
+    assert isinstance(lib.als_last_error(), bytes)
+
+
+def test_host_eigh_matches_numpy():
+    L, lib = _lib()
+    rng = np.random.default_rng(0)
+    for n in (1, 2, 7, 64, 128):
+        M = rng.standard_normal((n + 5, n))
+        A = np.ascontiguousarray(M.T @ M)
+        w = np.empty(n)
+        V = np.empty((n, n))
+        L.check(lib.als_host_eigh(n, L.ptr(A, C.c_double), L.ptr(w, C.c_double), L.ptr(V, C.c_double)))
+        ref = np.linalg.eigvalsh(A)
+        assert np.allclose(w, ref, rtol=1e-10, atol=1e-10 * ref.max())
+        assert np.allclose(V @ np.diag(w) @ V.T, A, atol=1e-9 * np.abs(A).max())
+        assert np.allclose(V.T @ V, np.eye(n), atol=1e-12)
+
+
+def test_spark_init_cpp_matches_oracle_bitwise():
+    from oracle import spark_als as O
+    L, lib = _lib()
+    us, it = C.c_int64(), C.c_int64()
+    L.check(lib.als_host_spark_side_seeds(42, C.byref(us), C.byref(it)))
+    pu, pi = O.spark_side_seeds(42)
+    assert (us.value, it.value) == (pu, pi)
+    ids = np.ascontiguousarray(np.array([-7, -3, 0, 1, 2, 5, 11, 12, 40, 99, 100, 2**31 - 1], dtype=np.int32))
+    for rank in (3, 10, 50):
+        out = np.empty((ids.size, rank), dtype=np.float32)
+        L.check(lib.als_host_spark_init(L.ptr(ids, C.c_int32), ids.size, rank, pu, 10, L.ptr(out, C.c_float)))
+        ref = O.spark_initialize(ids, rank, pu, 10)
+        assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+        assert np.allclose(np.linalg.norm(out, axis=1), 1.0, atol=1e-6)
+
+
+def test_plan_shards_balances_nnz():
+    L, lib = _lib()
+    rng = np.random.default_rng(3)
+    deg = rng.pareto(0.8, size=5000).astype(np.int64) + 1
+    ptr = np.ascontiguousarray(np.r_[0, np.cumsum(deg)])
+    for world in (1, 2, 3, 8):
+        st = np.empty(world + 1, dtype=np.int64)
+        L.check(lib.als_host_plan_shards(L.ptr(ptr, C.c_int64), deg.size, world, L.ptr(st, C.c_int64)))
+        assert st[0] == 0 and st[-1] == deg.size and np.all(np.diff(st) >= 0)
+        nnz = ptr[st[1:]] - ptr[st[:-1]]
+        assert nnz.sum() == ptr[-1]
+        assert nnz.max() <= ptr[-1] / world + deg.max() + 1
+
+
+def test_param_validation_messages_without_gpu():
+    from albedo_amd import ALS, IllegalArgumentException
+    with pytest.raises(IllegalArgumentException, match="rank given invalid value 0"):
+        ALS(rank=0)._context()
+    with pytest.raises(IllegalArgumentException, match="regParam given invalid value -1"):
+        ALS(regParam=-1.0)._context()
+    with pytest.raises(IllegalArgumentException, match="alpha"):
+        ALS(alpha=-0.5)._context()
+    with pytest.raises(IllegalArgumentException, match="maxIter"):
+        ALS(maxIter=-1)._context()
+    with pytest.raises(IllegalArgumentException, match="coldStartStrategy"):
+        ALS(coldStartStrategy="zero")
+    with pytest.raises(IllegalArgumentException, match="Integer range"):
+        ALS().fit({"user": np.array([1.5]), "item": np.array([1]), "rating": np.array([1.0])})
+    with pytest.raises(IllegalArgumentException, match="No ratings"):
+        ALS().fit({"user": np.array([], dtype=np.int32), "item": np.array([], dtype=np.int32),
+                   "rating": np.array([], dtype=np.float32)})
+
+
+def test_explain_params_and_setters():
+    from albedo_amd import ALS, SPARK_DEFAULT_SEED
+    als = (ALS().setImplicitPrefs(True).setRank(50).setRegParam(0.5).setAlpha(40).setMaxIter(26)
+           .setSeed(42).setColdStartStrategy("drop").setUserCol("user_id").setItemCol("repo_id")
+           .setRatingCol("starring"))
+    assert als.getRank() == 50 and als.getAlpha() == 40 and als.getUserCol() == "user_id"
+    assert "rank: rank of the factorization (default: 10, current: 50)" in als.explainParams()
+    assert ALS().getSeed() == SPARK_DEFAULT_SEED == 1994790107
+
+
+def test_no_device_fails_loudly_here():
+    """This container has no GPU: the engine must refuse, never fall back to the CPU."""
+    from albedo_amd import _lib as L
+    from albedo_amd import ALS
+    if L.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(L.ALSError) as ei:
+        ALS(rank=4).fit({"user": np.array([1, 2]), "item": np.array([1, 1]), "rating": np.array([1.0, 1.0])})
+    assert ei.value.code == L.ALS_E_NO_DEVICE
