@@ -258,24 +258,36 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
     colB[I] = __shfl(colE, 16 * I + i16);
     vB[I] = __shfl((int)valid, 16 * I + i16) != 0;
   }
+  constexpr int NC = KP / 16;
+  constexpr bool KEEPZ = D <= 32;  // keep the gathered rows in registers for the x' epilogue
+  f32x4 zf[KEEPZ ? NB : 1][KEEPZ ? NC : 1];
+  if constexpr (KEEPZ) {  // issue every gather up front: one latency for the whole row
+#pragma unroll
+    for (int I = 0; I < NB; ++I)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) zf[I][c] = vB[I] ? ld4(a.Z + (int64_t)colB[I] * KP + 16 * c + 4 * g) : zero4();
+  }
   f32x4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = zero4();
   bool bad = false;
-  for (int c0 = 0; c0 < KP; c0 += 16) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int c0 = 16 * c;
     const f32x4 dl = ld4(a.lam + c0 + 4 * g);
     float sd[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      const int c = c0 + 4 * g + m;
+      const int cc = c0 + 4 * g + m;
       const float dd = dl[m] + lamn;
-      if (c < a.kreal && !(dd > 0.f)) bad = true;
-      sd[m] = (c < a.kreal && dd > 0.f) ? 1.0f / sqrtf(dd) : 0.f;
+      if (cc < a.kreal && !(dd > 0.f)) bad = true;
+      sd[m] = (cc < a.kreal && dd > 0.f) ? 1.0f / sqrtf(dd) : 0.f;
     }
     f32x4 z[NB];
 #pragma unroll
     for (int I = 0; I < NB; ++I) {
-      z[I] = vB[I] ? ld4(a.Z + (int64_t)colB[I] * KP + c0 + 4 * g) : zero4();
+      if constexpr (KEEPZ) z[I] = zf[I][c];
+      else z[I] = vB[I] ? ld4(a.Z + (int64_t)colB[I] * KP + c0 + 4 * g) : zero4();
 #pragma unroll
       for (int m = 0; m < 4; ++m) z[I][m] *= sd[m];
     }
@@ -343,24 +355,60 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
     const float vc = rdlane(y * dg, c);
     y = (me < c) ? fmaf(-lt[c], vc, y) : ((me == c) ? vc : y);
   }
-  // x' = D⁻¹ Zᵀ v ; lanes own columns lane + 64h
-  float xacc[NHC];
+  // x' = D⁻¹ Zᵀ v
+  if constexpr (KEEPZ) {
+    // lane (i16, g) holds Z[entry 16I+i16][16c+4g+m]: scale by v, sum over I in-lane and over the
+    // 16 entry lanes of its group by xor-shuffles, lane i16 == 0 of each group stores 4 columns
+    float vI[NB];
 #pragma unroll
-  for (int h = 0; h < NHC; ++h) xacc[h] = 0.f;
-  for (int e = 0; e < d; ++e) {
-    const float ve = rdlane(y, e);
-    const int ce_col = rdlane_i(colE, e);
-    if (ve != 0.f) {
-      const float* zr = a.Z + (int64_t)ce_col * KP + lane;
+    for (int I = 0; I < NB; ++I) vI[I] = __shfl(y, 16 * I + i16);
 #pragma unroll
-      for (int h = 0; h < NHC; ++h) xacc[h] = fmaf(ve, zr[64 * h], xacc[h]);
+    for (int c = 0; c < NC; ++c) {
+      f32x4 pr = zf[0][c] * vI[0];
+#pragma unroll
+      for (int I = 1; I < NB; ++I) pr += zf[I][c] * vI[I];
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) pr[m] += __shfl_xor(pr[m], o);
+      if (i16 == 0) {
+        const f32x4 dl = ld4(a.lam + 16 * c + 4 * g);
+        f32x4 o4;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int cc = 16 * c + 4 * g + m;
+          const float dd = dl[m] + lamn;
+          o4[m] = (cc < a.kreal && dd > 0.f) ? pr[m] / dd : 0.f;
+        }
+        *reinterpret_cast<f32x4*>(a.X + (int64_t)j * KP + 16 * c + 4 * g) = o4;
+      }
     }
-  }
+  } else {
+    // lanes own columns lane + 64h; gathers issued 8 entries at a time
+    float xacc[NHC];
 #pragma unroll
-  for (int h = 0; h < NHC; ++h) {
-    const int c = lane + 64 * h;
-    const float dd = a.lam[c] + lamn;
-    a.X[(int64_t)j * KP + c] = (c < a.kreal && dd > 0.f) ? xacc[h] / dd : 0.f;
+    for (int h = 0; h < NHC; ++h) xacc[h] = 0.f;
+    for (int e0 = 0; e0 < d; e0 += 8) {
+      float ve[8], zz[8][NHC];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u < d ? e0 + u : d - 1;
+        ve[u] = e0 + u < d ? rdlane(y, e) : 0.f;
+        const float* zr = a.Z + (int64_t)rdlane_i(colE, e) * KP + lane;
+#pragma unroll
+        for (int h = 0; h < NHC; ++h) zz[u][h] = zr[64 * h];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int h = 0; h < NHC; ++h) xacc[h] = fmaf(ve[u], zz[u][h], xacc[h]);
+    }
+#pragma unroll
+    for (int h = 0; h < NHC; ++h) {
+      const int c = lane + 64 * h;
+      const float dd = a.lam[c] + lamn;
+      a.X[(int64_t)j * KP + c] = (c < a.kreal && dd > 0.f) ? xacc[h] / dd : 0.f;
+    }
   }
 }
 
@@ -376,14 +424,41 @@ hipError_t launch_solve_light(int KP, int D, const SolveArgs& a, hipStream_t s) 
 }
 
 // =============================================================================================
-// Heavy rows: explicit A' = diag(Λ + λn) + Σ c z zᵀ, b' = Σ w z (MFMA, permuted 16-col blocks),
-// blocked Cholesky (16-wide panels; TRSM per row; SYRK on MFMA) with b' carried as row KP
-// (forward substitution for free), blocked back substitution.  One workgroup per dst row.
+// Heavy rows: explicit A' = diag(Λ + λn) + Σ c z zᵀ, b' = Σ w z, then Cholesky + substitutions.
+// One 256-thread workgroup per dst row, sized for 4 workgroups per CU (LDS <= 40 KiB):
+//  build   the row's Z rows are gathered 32 at a time into a double-buffered LDS stage shared by
+//          the 4 waves (one barrier per 32 ratings); each wave owns a fixed set of upper 16x16
+//          tiles (permuted column blocks: one ds_read_b128 per lane per 64 columns) and
+//          accumulates them with v_mfma_f32_16x16x4_f32 on √c-scaled rows (bitwise symmetric).
+//  store   the tiles go to LDS as packed lower-triangular 16x17 tiles (the stage is dead by then).
+//  factor  right-looking, 16-wide panels, two barriers per panel: the waves that own panel rows
+//          factor the 16x16 diagonal tile redundantly in registers and solve their rows against
+//          it with wave-uniform (SGPR) broadcasts of L11; the trailing update runs on MFMA.  b' is
+//          carried as an extra row, so the forward substitution comes for free.
+//  back    Lᵀx = y by one wave, no barriers.
 // =============================================================================================
+constexpr int HT_LD = 17, HT_SZ = 16 * HT_LD;
+__device__ __forceinline__ int htile(int I, int J) { return (I * (I + 1) / 2 + J) * HT_SZ; }
+__device__ __forceinline__ int hel(int r, int c) { return htile(r >> 4, c >> 4) + (r & 15) * HT_LD + (c & 15); }
+
+template <int KP>
+struct HeavyLds {
+  static constexpr int NB = KP / 16, NTL = NB * (NB + 1) / 2;
+  static constexpr int TILES = NTL * HT_SZ, STAGE = 2 * 32 * KP;
+  static constexpr int BIG = TILES > STAGE ? TILES : STAGE;
+  static constexpr int OFF_B = BIG, OFF_DIAG = OFF_B + KP, OFF_W = OFF_DIAG + KP, OFF_FLAG = OFF_W + 128;
+  static constexpr int FLOATS = OFF_FLAG + 4;
+};
+
 template <int KP, int W>
-__device__ __forceinline__ void heavy_build(const SolveArgs& a, int64_t p0, int d, float* A, int* s_npos) {
-  constexpr int NQ = KP / 16, NT = NQ * (NQ + 1) / 2, NTW = (NT + 3) / 4, NH = KP / 64, LDA = KP + 1;
-  const int lane = threadIdx.x & 63, g = lane >> 4, i16 = lane & 15;
+__device__ __forceinline__ void heavy_build(const SolveArgs& a, int64_t p0, int d, float* smem) {
+  using Lay = HeavyLds<KP>;
+  constexpr int NQ = KP / 16, NT = NQ * (NQ + 1) / 2, NTW = (NT + 3) / 4, NH = KP / 64;
+  constexpr int F4ROW = KP / 4, RPP = 256 / F4ROW, NPASS = 32 / RPP;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i16 = lane & 15;
+  float* stage = smem;
+  float* sw = smem + Lay::OFF_W;  // [buf][0..31] = sqrt(c), [buf][32..63] = w
+  const int prow = tid / F4ROW, pch = (tid % F4ROW) * 4;
   f32x4 acc[NTW];
 #pragma unroll
   for (int s = 0; s < NTW; ++s) acc[s] = zero4();
@@ -391,67 +466,69 @@ __device__ __forceinline__ void heavy_build(const SolveArgs& a, int64_t p0, int 
 #pragma unroll
   for (int h = 0; h < NH; ++h) bacc[h] = zero4();
   int npos = 0;
-  // 1-deep register prefetch of the next 4 entries
-  auto fetch = [&](int e0, f32x4* zv, float& sc, float& w, int& pos) {
-    const int e = e0 + g;
-    float r = 0.f, c = 0.f;
-    w = 0.f;
-    pos = 0;
-    if (e < d) {
-      r = a.val[p0 + e];
-      rating_weights(r, a.implicit, a.alpha, c, w);
-      pos = r > 0.f ? 1 : 0;
-      const float* zr = a.Z + (int64_t)a.col[p0 + e] * KP + 4 * i16;
+  f32x4 stg[NPASS];
+  float wsc = 0.f, ww = 0.f;
+  auto gload = [&](int e0) {
+    int cix[NPASS];
 #pragma unroll
-      for (int h = 0; h < NH; ++h) zv[h] = ld4(zr + 64 * h);
-    } else {
-#pragma unroll
-      for (int h = 0; h < NH; ++h) zv[h] = zero4();
+    for (int p = 0; p < NPASS; ++p) {
+      const int e = e0 + p * RPP + prow;
+      cix[p] = e < d ? a.col[p0 + e] : -1;
     }
-    sc = sqrtf(c);
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) stg[p] = cix[p] >= 0 ? ld4(a.Z + (int64_t)cix[p] * KP + pch) : zero4();
+    if (tid < 32) {
+      const int e = e0 + tid;
+      float r = 0.f, c = 0.f, w = 0.f;
+      if (e < d) {
+        r = a.val[p0 + e];
+        rating_weights(r, a.implicit, a.alpha, c, w);
+        npos += r > 0.f ? 1 : 0;
+      }
+      wsc = sqrtf(c);
+      ww = w;
+    }
   };
-  f32x4 zc[NH], zn[NH];
-  float scc, wc, scn, wn;
-  int posc, posn;
-  fetch(0, zc, scc, wc, posc);
-  for (int e0 = 0; e0 < d; e0 += 4) {
-    if (e0 + 4 < d) fetch(e0 + 4, zn, scn, wn, posn);
-    f32x4 zs[NH];
+  auto lds_put = [&](int buf) {
 #pragma unroll
-    for (int h = 0; h < NH; ++h) zs[h] = zc[h] * scc;
-    if (W == 0) {
-#pragma unroll
-      for (int h = 0; h < NH; ++h) bacc[h] += zc[h] * wc;
-      npos += __popcll(__ballot(i16 == 0 && posc));
+    for (int p = 0; p < NPASS; ++p)
+      *reinterpret_cast<f32x4*>(stage + (buf * 32 + p * RPP + prow) * KP + pch) = stg[p];
+    if (tid < 32) {
+      sw[buf * 64 + tid] = wsc;
+      sw[buf * 64 + 32 + tid] = ww;
     }
-    static_for<0, NTW>([&](auto s) {
-      constexpr int t = W + 4 * decltype(s)::value;
-      if constexpr (t < NT) {
-        constexpr TilePair p = upper_tile(t, NQ);
-        acc[s] = mfma4(zs[p.a >> 2][p.a & 3], zs[p.b >> 2][p.b & 3], acc[s]);
+  };
+  gload(0);
+  lds_put(0);
+  __syncthreads();
+  const int nst = (d + 31) / 32;
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nst) gload((st + 1) * 32);
+    const float* sb = stage + buf * 32 * KP;
+#pragma unroll 2
+    for (int q = 0; q < 8; ++q) {
+      const int row = 4 * q + g;
+      const float sc = sw[buf * 64 + row];
+      f32x4 zs[NH];
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        const f32x4 zv = *reinterpret_cast<const f32x4*>(sb + row * KP + 64 * h + 4 * i16);
+        zs[h] = zv * sc;
+        if (W == 0) bacc[h] += zv * sw[buf * 64 + 32 + row];
       }
-    });
-#pragma unroll
-    for (int h = 0; h < NH; ++h) zc[h] = zn[h];
-    scc = scn; wc = wn; posc = posn;
-  }
-  if (W == 0) {
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        bacc[h][m] += __shfl_xor(bacc[h][m], 16);
-        bacc[h][m] += __shfl_xor(bacc[h][m], 32);
-      }
+      static_for<0, NTW>([&](auto s) {
+        constexpr int t = W + 4 * decltype(s)::value;
+        if constexpr (t < NT) {
+          constexpr TilePair p = upper_tile(t, NQ);
+          acc[s] = mfma4(zs[p.a >> 2][p.a & 3], zs[p.b >> 2][p.b & 3], acc[s]);
+        }
+      });
     }
-    if (lane < 16) {
-#pragma unroll
-      for (int h = 0; h < NH; ++h)
-        for (int m = 0; m < 4; ++m) A[KP * LDA + 64 * h + 4 * lane + m] = bacc[h][m];
-    }
-    if (lane == 0) *s_npos = a.implicit ? npos : d;
+    if (st + 1 < nst) lds_put(buf ^ 1);
+    __syncthreads();
   }
-  // lower triangle of A' (diagonal term added after the barrier)
+  // stage is dead: store the lower triangle into packed tiles, b' into its vector
   static_for<0, NTW>([&](auto s) {
     constexpr int t = W + 4 * decltype(s)::value;
     if constexpr (t < NT) {
@@ -461,145 +538,163 @@ __device__ __forceinline__ void heavy_build(const SolveArgs& a, int64_t p0, int 
         const int i = 4 * g + r, jj = i16;
         if (p.a != p.b || i >= jj) {
           const int c1 = pcol(p.a, i), c2 = pcol(p.b, jj);
-          const int hi = c1 > c2 ? c1 : c2, lo = c1 > c2 ? c2 : c1;
-          A[hi * LDA + lo] = acc[s][r];
+          smem[c1 > c2 ? hel(c1, c2) : hel(c2, c1)] = acc[s][r];
         }
       }
     }
   });
+  if (W == 0) {
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        bacc[h][m] += __shfl_xor(bacc[h][m], 16);
+        bacc[h][m] += __shfl_xor(bacc[h][m], 32);
+      }
+    if (lane < 16) {
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) smem[Lay::OFF_B + 64 * h + 4 * lane + m] = bacc[h][m];
+    }
+    // npos lives in lanes 0..31 of wave 0
+    for (int o = 16; o > 0; o >>= 1) npos += __shfl_xor(npos, o);
+    if (lane == 0) reinterpret_cast<int*>(smem + Lay::OFF_FLAG)[0] = a.implicit ? npos : d;
+  }
+}
+
+// 16x16 Cholesky of the diagonal tile in registers (lane i16 = row i16).  dg = 1/L[i16][i16].
+__device__ __forceinline__ bool chol16(float (&rr)[16], float& dg, int i) {
+  bool notpd = false;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const float piv = rdlane(rr[c], c);
+    if (!(piv > 0.f)) notpd = true;
+    const float s = sqrtf(piv), inv = 1.0f / s;
+    rr[c] = (i == c) ? s : rr[c] * inv;
+    dg = (i == c) ? inv : dg;
+#pragma unroll
+    for (int m = c + 1; m < 16; ++m) rr[m] = fmaf(-rr[c], rdlane(rr[c], m), rr[m]);
+  }
+  return notpd;
 }
 
 template <int KP>
-__global__ __launch_bounds__(256) void solve_heavy_kernel(SolveArgs a) {
-  constexpr int LDA = KP + 1, NB = KP / 16;
+__global__ __launch_bounds__(256, 4) void solve_heavy_kernel(SolveArgs a) {
+  using Lay = HeavyLds<KP>;
+  constexpr int NB = KP / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* A = smem;                        // (KP+1) x LDA, row KP = b' / y / x
-  float* sdiag = smem + (KP + 1) * LDA;   // 1/L[c][c]
-  int* s_flag = reinterpret_cast<int*>(sdiag + KP);  // [0] npos, [1] error bits
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* bvec = smem + Lay::OFF_B;
+  float* sdiag = smem + Lay::OFF_DIAG;
+  int* s_flag = reinterpret_cast<int*>(smem + Lay::OFF_FLAG);  // [0] npos, [1] error bits
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, i16 = lane & 15;
   const int j = a.rows[blockIdx.x];
   const int64_t p0 = a.ptr[j];
   const int d = (int)(a.ptr[j + 1] - p0);
   if (tid == 0) s_flag[1] = 0;
-  if (wave == 0) heavy_build<KP, 0>(a, p0, d, A, s_flag);
-  else if (wave == 1) heavy_build<KP, 1>(a, p0, d, A, s_flag);
-  else if (wave == 2) heavy_build<KP, 2>(a, p0, d, A, s_flag);
-  else heavy_build<KP, 3>(a, p0, d, A, s_flag);
+  if (wave == 0) heavy_build<KP, 0>(a, p0, d, smem);
+  else if (wave == 1) heavy_build<KP, 1>(a, p0, d, smem);
+  else if (wave == 2) heavy_build<KP, 2>(a, p0, d, smem);
+  else heavy_build<KP, 3>(a, p0, d, smem);
   __syncthreads();
   const float lamn = a.reg * (float)s_flag[0];
-  for (int c = tid; c < KP; c += 256) {
-    const float dd = c < a.kreal ? a.lam[c] + lamn : 1.0f;
-    A[c * LDA + c] += c < a.kreal ? dd : 1.0f;
-  }
+  for (int c = tid; c < KP; c += 256) smem[hel(c, c)] += c < a.kreal ? a.lam[c] + lamn : 1.0f;
   __syncthreads();
   for (int jb = 0; jb < NB; ++jb) {
     const int j0 = 16 * jb;
-    if (wave == 0) {  // factor the 16x16 diagonal block in registers
-      const int i = lane & 15;
-      float rr[16];
+    const int nrow = KP - j0 - 16 + 1;  // rows below the panel + the b' row
+    float rr[16];
+    float dg = 1.f;
+    bool notpd = false;
+    if (wave * 64 < nrow) {
 #pragma unroll
-      for (int m = 0; m < 16; ++m) rr[m] = A[(j0 + i) * LDA + j0 + m];
-      bool notpd = false;
+      for (int m = 0; m < 16; ++m) rr[m] = smem[htile(jb, jb) + i16 * HT_LD + m];
+      notpd = chol16(rr, dg, i16);
+      const int ridx = wave * 64 + lane;
+      if (ridx < nrow) {  // L21 row = A21 row · L11⁻ᵀ with L11 broadcast from the registers
+        const int i = j0 + 16 + ridx;
+        float* src = i < KP ? smem + htile(i >> 4, jb) + (i & 15) * HT_LD : bvec + j0;
+        float x[16];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const float piv = rdlane(rr[c], c);
-        if (!(piv > 0.f)) notpd = true;
-        const float s = sqrtf(piv), inv = 1.0f / s;
-        rr[c] = (i == c) ? s : rr[c] * inv;
+        for (int m = 0; m < 16; ++m) x[m] = src[m];
 #pragma unroll
-        for (int m = c + 1; m < 16; ++m) rr[m] = fmaf(-rr[c], rdlane(rr[c], m), rr[m]);
-      }
-      if (lane < 16) {
+        for (int c = 0; c < 16; ++c) {
+          float s = x[c];
 #pragma unroll
-        for (int m = 0; m < 16; ++m) {
-          if (m <= i) A[(j0 + i) * LDA + j0 + m] = rr[m];
-          if (m == i) sdiag[j0 + i] = 1.0f / rr[m];
+          for (int m = 0; m < c; ++m) s = fmaf(-x[m], rdlane(rr[m], c), s);
+          x[c] = s * rdlane(dg, c);
         }
+#pragma unroll
+        for (int m = 0; m < 16; ++m) src[m] = x[m];
       }
-      if (notpd && lane == 0) s_flag[1] = 2;
     }
     __syncthreads();
-    // TRSM: rows below the block (and the b' row) : L21 = A21 L11⁻ᵀ
-    const int nrow = KP + 1 - j0 - 16;
-    if (tid < nrow) {
-      const int i = j0 + 16 + tid;
-      float x[16];
+    if (wave == 0 && lane < 16) {  // L11 back into its tile (read again only by the back substitution)
 #pragma unroll
-      for (int m = 0; m < 16; ++m) x[m] = A[i * LDA + j0 + m];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        float s = x[c];
-#pragma unroll
-        for (int m = 0; m < c; ++m) s = fmaf(-x[m], A[(j0 + c) * LDA + j0 + m], s);
-        x[c] = s * sdiag[j0 + c];
-      }
-#pragma unroll
-      for (int m = 0; m < 16; ++m) A[i * LDA + j0 + m] = x[m];
+      for (int m = 0; m < 16; ++m)
+        if (m <= i16) smem[htile(jb, jb) + i16 * HT_LD + m] = rr[m];
+      sdiag[j0 + i16] = dg;
+      if (notpd) s_flag[1] = 2;
     }
-    __syncthreads();
-    // SYRK on the trailing lower triangle (MFMA), and the b' row update (VALU)
     const int nrem = NB - jb - 1;
     const int ntr = nrem * (nrem + 1) / 2;
-    const int g = lane >> 4, i16 = lane & 15;
     for (int t = wave; t < ntr; t += 4) {
       int ti = 0, tt = t;  // lower tiles (I >= M), row-major
       while (tt > ti) { tt -= ti + 1; ++ti; }
       const int I = jb + 1 + ti, M = jb + 1 + tt;
+      float* ct = smem + htile(I, M);
+      const float* at = smem + htile(I, jb) + i16 * HT_LD + g;
+      const float* bt = smem + htile(M, jb) + i16 * HT_LD + g;
       f32x4 acc;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = A[(16 * I + 4 * g + r) * LDA + 16 * M + i16];
+      for (int r = 0; r < 4; ++r) acc[r] = ct[(4 * g + r) * HT_LD + i16];
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const float av = -A[(16 * I + i16) * LDA + j0 + 4 * s4 + g];
-        const float bv = A[(16 * M + i16) * LDA + j0 + 4 * s4 + g];
-        acc = mfma4(av, bv, acc);
-      }
+      for (int s4 = 0; s4 < 4; ++s4) acc = mfma4(-at[4 * s4], bt[4 * s4], acc);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) A[(16 * I + 4 * g + r) * LDA + 16 * M + i16] = acc[r];
+      for (int r = 0; r < 4; ++r) ct[(4 * g + r) * HT_LD + i16] = acc[r];
     }
     for (int m = j0 + 16 + tid; m < KP; m += 256) {
-      float s = A[KP * LDA + m];
+      float s = bvec[m];
+      const float* lr = smem + htile(m >> 4, jb) + (m & 15) * HT_LD;
 #pragma unroll
-      for (int c = 0; c < 16; ++c) s = fmaf(-A[KP * LDA + j0 + c], A[m * LDA + j0 + c], s);
-      A[KP * LDA + m] = s;
+      for (int c = 0; c < 16; ++c) s = fmaf(-bvec[j0 + c], lr[c], s);
+      bvec[m] = s;
     }
     __syncthreads();
   }
-  // back substitution Lᵀ x = y
-  for (int jb = NB - 1; jb >= 0; --jb) {
-    const int j0 = 16 * jb;
-    if (wave == 0) {
-      const int q = lane & 15;
-      float yv = A[KP * LDA + j0 + q];
-      const float sdq = sdiag[j0 + q];
+  if (wave == 0) {  // back substitution Lᵀ x = y, single wave
+    for (int jb = NB - 1; jb >= 0; --jb) {
+      const int j0 = 16 * jb;
+      float yv = bvec[j0 + i16];
+      const float sdq = sdiag[j0 + i16];
       float lcol[16];
 #pragma unroll
-      for (int m = 0; m < 16; ++m) lcol[m] = A[(j0 + m) * LDA + j0 + q];
+      for (int m = 0; m < 16; ++m) lcol[m] = smem[htile(jb, jb) + m * HT_LD + i16];
 #pragma unroll
       for (int i = 15; i >= 0; --i) {
         const float xi = rdlane(yv * sdq, i);
-        yv = (q < i) ? fmaf(-lcol[i], xi, yv) : ((q == i) ? xi : yv);
+        yv = (i16 < i) ? fmaf(-lcol[i], xi, yv) : ((i16 == i) ? xi : yv);
       }
-      if (lane < 16) A[KP * LDA + j0 + q] = yv;
-    }
-    __syncthreads();
-    for (int m = tid; m < j0; m += 256) {
-      float s = A[KP * LDA + m];
+      if (lane < 16) bvec[j0 + i16] = yv;
+      WAVE_LDS_SYNC();
+      for (int m = lane; m < j0; m += 64) {
+        float s = bvec[m];
+        const float* lt = smem + htile(jb, m >> 4) + (m & 15);
 #pragma unroll
-      for (int c = 0; c < 16; ++c) s = fmaf(-A[(j0 + c) * LDA + m], A[KP * LDA + j0 + c], s);
-      A[KP * LDA + m] = s;
+        for (int c = 0; c < 16; ++c) s = fmaf(-lt[c * HT_LD], bvec[j0 + c], s);
+        bvec[m] = s;
+      }
+      WAVE_LDS_SYNC();
     }
-    __syncthreads();
+    for (int c = lane; c < KP; c += 64) a.X[(int64_t)j * KP + c] = c < a.kreal ? bvec[c] : 0.f;
+    if (lane == 0 && s_flag[1]) atomicOr(a.err, s_flag[1]);
   }
-  for (int c = tid; c < KP; c += 256) a.X[(int64_t)j * KP + c] = c < a.kreal ? A[KP * LDA + c] : 0.f;
-  if (tid == 0 && s_flag[1]) atomicOr(a.err, s_flag[1]);
 }
 
 hipError_t launch_solve_heavy(int KP, const SolveArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;
-  const size_t lds = ((size_t)(KP + 1) * (KP + 1) + KP + 4) * sizeof(float);
-  if (KP == 64) solve_heavy_kernel<64><<<(int)a.n_rows, 256, lds, s>>>(a);
-  else if (KP == 128) solve_heavy_kernel<128><<<(int)a.n_rows, 256, lds, s>>>(a);
+  if (KP == 64) solve_heavy_kernel<64><<<(int)a.n_rows, 256, HeavyLds<64>::FLOATS * 4, s>>>(a);
+  else if (KP == 128) solve_heavy_kernel<128><<<(int)a.n_rows, 256, HeavyLds<128>::FLOATS * 4, s>>>(a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
