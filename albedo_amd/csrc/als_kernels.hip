@@ -35,6 +35,10 @@ __device__ __forceinline__ float rdlane(float x, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
 }
 __device__ __forceinline__ int rdlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+// v_rsq_f32 / v_rcp_f32 / v_sqrt_f32: single instructions (~1 ulp) instead of the IEEE-exact
+// multi-instruction expansions; the solve tolerance is 1e-4 relative (tests state it)
+__device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
@@ -281,7 +285,7 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
       const int cc = c0 + 4 * g + m;
       const float dd = dl[m] + lamn;
       if (cc < a.kreal && !(dd > 0.f)) bad = true;
-      sd[m] = (cc < a.kreal && dd > 0.f) ? 1.0f / sqrtf(dd) : 0.f;
+      sd[m] = (cc < a.kreal && dd > 0.f) ? frsq(dd) : 0.f;
     }
     f32x4 z[NB];
 #pragma unroll
@@ -312,11 +316,12 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
   });
   WAVE_LDS_SYNC();
   const int me = lane < D ? lane : 0;
+  const float cinv = valid ? frcp(ce) : 0.f;
   float kr[D];
 #pragma unroll
   for (int m = 0; m < D; ++m) {
     const float v = Ks[me * LDK + m];
-    kr[m] = (m == me) ? (valid ? v + 1.0f / ce : 1.0f) : (valid ? v : 0.0f);
+    kr[m] = (m == me) ? (valid ? v + cinv : 1.0f) : (valid ? v : 0.0f);
   }
   // Cholesky K = L Lᵀ, lane i holds row i (entries m <= i are L[i][m] when done)
   bool notpd = false;
@@ -325,7 +330,7 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
   for (int c = 0; c < D; ++c) {
     const float piv = rdlane(kr[c], c);
     if (!(piv > 0.f)) notpd = true;
-    const float s = sqrtf(piv), inv = 1.0f / s;
+    const float inv = frsq(piv), s = piv * inv;
     kr[c] = (me == c) ? s : kr[c] * inv;
     dg = (me == c) ? inv : dg;
 #pragma unroll
@@ -333,7 +338,7 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
   }
   if (notpd && lane == 0) atomicOr(a.err, 2);
   // forward: L y = C⁻¹ w
-  float y = valid ? we / ce : 0.f;
+  float y = valid ? we * cinv : 0.f;
 #pragma unroll
   for (int c = 0; c < D; ++c) {
     const float yc = rdlane(y * dg, c);
@@ -378,7 +383,7 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
         for (int m = 0; m < 4; ++m) {
           const int cc = 16 * c + 4 * g + m;
           const float dd = dl[m] + lamn;
-          o4[m] = (cc < a.kreal && dd > 0.f) ? pr[m] / dd : 0.f;
+          o4[m] = (cc < a.kreal && dd > 0.f) ? pr[m] * frcp(dd) : 0.f;
         }
         *reinterpret_cast<f32x4*>(a.X + (int64_t)j * KP + 16 * c + 4 * g) = o4;
       }
@@ -407,7 +412,7 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
     for (int h = 0; h < NHC; ++h) {
       const int c = lane + 64 * h;
       const float dd = a.lam[c] + lamn;
-      a.X[(int64_t)j * KP + c] = (c < a.kreal && dd > 0.f) ? xacc[h] / dd : 0.f;
+      a.X[(int64_t)j * KP + c] = (c < a.kreal && dd > 0.f) ? xacc[h] * frcp(dd) : 0.f;
     }
   }
 }
@@ -564,13 +569,18 @@ __device__ __forceinline__ void heavy_build(const SolveArgs& a, int64_t p0, int 
 }
 
 // 16x16 Cholesky of the diagonal tile in registers (lane i16 = row i16).  dg = 1/L[i16][i16].
+// A pivot that collapses below 2^-21 of its panel-start value is numerically singular in fp32
+// (Spark's fp64 dppsv reports info > 0 on such systems); it is reported as not positive definite.
 __device__ __forceinline__ bool chol16(float (&rr)[16], float& dg, int i) {
   bool notpd = false;
+  float dstart[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) dstart[c] = rdlane(rr[c], c);
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
     const float piv = rdlane(rr[c], c);
-    if (!(piv > 0.f)) notpd = true;
-    const float s = sqrtf(piv), inv = 1.0f / s;
+    if (!(piv > dstart[c] * 4.76837158e-07f)) notpd = true;
+    const float inv = frsq(piv), s = piv * inv;
     rr[c] = (i == c) ? s : rr[c] * inv;
     dg = (i == c) ? inv : dg;
 #pragma unroll
@@ -619,10 +629,9 @@ __global__ __launch_bounds__(256, 4) void solve_heavy_kernel(SolveArgs a) {
         for (int m = 0; m < 16; ++m) x[m] = src[m];
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
-          float s = x[c];
+          x[c] *= rdlane(dg, c);
 #pragma unroll
-          for (int m = 0; m < c; ++m) s = fmaf(-x[m], rdlane(rr[m], c), s);
-          x[c] = s * rdlane(dg, c);
+          for (int m = c + 1; m < 16; ++m) x[m] = fmaf(-x[c], rdlane(rr[c], m), x[m]);
         }
 #pragma unroll
         for (int m = 0; m < 16; ++m) src[m] = x[m];
@@ -686,7 +695,13 @@ __global__ __launch_bounds__(256, 4) void solve_heavy_kernel(SolveArgs a) {
       }
       WAVE_LDS_SYNC();
     }
-    for (int c = lane; c < KP; c += 64) a.X[(int64_t)j * KP + c] = c < a.kreal ? bvec[c] : 0.f;
+    bool nonfinite = false;
+    for (int c = lane; c < KP; c += 64) {
+      const float v = c < a.kreal ? bvec[c] : 0.f;
+      nonfinite |= !isfinite(v);
+      a.X[(int64_t)j * KP + c] = v;
+    }
+    if (__any(nonfinite)) s_flag[1] |= 2;
     if (lane == 0 && s_flag[1]) atomicOr(a.err, s_flag[1]);
   }
 }
