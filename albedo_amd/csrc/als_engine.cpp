@@ -120,7 +120,7 @@ struct als_ctx {
   int64_t nnz = 0;
   bool has_ratings = false;
   bool model_only = false;
-  DevBuf slab, d_G, d_P, d_lam, d_err;
+  DevBuf slab, d_G, d_P, d_lam, d_err, d_Gt;
   int slab_blocks = 0;
   hipEvent_t ev[8] = {};
 };
@@ -349,6 +349,76 @@ float event_ms(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
+// nonnegative = true: Spark's NNLSSolver in the original basis (no rotation; B stays I)
+int half_sweep_nnls(als_ctx* c, int t) {
+  const int sidx = 1 - t;
+  Side& S = c->s[sidx];
+  Side& T = c->s[t];
+  const int KP = c->KP, k = c->p.rank;
+  hipStream_t st = c->st;
+  hipEvent_t* ev = c->ev;
+  float* zown = S.d_Z.as<float>() + (size_t)c->rank * S.maxrows * KP;
+  const int ngt = nnls_gtile_floats(KP);
+  std::vector<float> gt(ngt, 0.f);
+  if (c->p.implicit_prefs) {
+    HIPCHK(launch_gram(KP, S.d_X.as<float>(), S.own_n, c->slab.as<double>(), c->slab_blocks, c->d_G.as<double>(), st));
+    TRYC(allreduce_G(c));
+    std::vector<double> Gf((size_t)KP * KP);
+    HIPCHK(hipMemcpyAsync(Gf.data(), c->d_G.p, Gf.size() * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    S.G.assign((size_t)k * k, 0.0);
+    for (int i = 0; i < k; ++i)
+      for (int j = 0; j < k; ++j) S.G[(size_t)i * k + j] = Gf[(size_t)i * KP + j];
+    for (int i = 0; i < KP; ++i)
+      for (int j = 0; j <= i; ++j) gt[nnls_gtile_index(i, j)] = (float)Gf[(size_t)i * KP + j];
+  }
+  HIPCHK(hipEventRecord(ev[1], st));
+  HIPCHK(c->d_Gt.ensure((size_t)ngt * 4));
+  HIPCHK(hipMemcpyAsync(c->d_Gt.p, gt.data(), (size_t)ngt * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(c->d_lam.p, 0, KP * 4, st));
+  HIPCHK(hipEventRecord(ev[2], st));
+  HIPCHK(hipMemcpyAsync(zown, S.d_X.p, (size_t)S.own_n * KP * 4, hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipEventRecord(ev[3], st));
+  TRYC(allgather_rows(c, S.d_Z.as<float>(), S.maxrows));
+  HIPCHK(hipEventRecord(ev[4], st));
+  HIPCHK(hipMemsetAsync(c->d_err.p, 0, 4, st));
+  HIPCHK(hipEventRecord(ev[5], st));
+  SolveArgs a{};
+  a.Z = S.d_Z.as<float>();
+  a.ptr = T.d_ptr.as<int64_t>();
+  a.col = T.d_col.as<int32_t>();
+  a.val = T.d_val.as<float>();
+  a.lam = c->d_lam.as<float>();
+  a.X = T.d_X.as<float>();
+  a.kreal = k;
+  a.implicit = c->p.implicit_prefs;
+  a.alpha = (float)c->p.alpha;
+  a.reg = (float)c->p.reg_param;
+  a.err = c->d_err.as<int>();
+  a.rows = T.d_rows.as<int32_t>();
+  a.n_rows = T.boff[NBUCKET];
+  HIPCHK(launch_solve_nnls(KP, a, c->d_Gt.as<float>(), st));
+  T.stats[0] = T.stats[1] = 0;
+  T.stats[2] = a.n_rows;
+  T.stats[3] = T.own_nnz;
+  HIPCHK(hipEventRecord(ev[6], st));
+  int err = 0;
+  HIPCHK(hipMemcpyAsync(&err, c->d_err.p, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  T.t[ALS_T_GRAM] = event_ms(ev[0], ev[1]);
+  T.t[ALS_T_EIG] = 0.0;
+  T.t[ALS_T_ROTATE] = event_ms(ev[2], ev[3]);
+  T.t[ALS_T_COMM] = event_ms(ev[3], ev[4]);
+  T.t[ALS_T_SOLVE_LIGHT] = 0.0;
+  T.t[ALS_T_SOLVE_HEAVY] = event_ms(ev[5], ev[6]);
+  T.t[ALS_T_HALF_TOTAL] = event_ms(ev[0], ev[6]);
+  if (err) return fail(ALS_E_NOT_POSITIVE_DEFINITE, "NNLS solve produced a non-finite result");
+  T.B = S.B;
+  T.has_factors = true;
+  T.orig_valid = false;
+  return ALS_OK;
+}
+
 int half_sweep(als_ctx* c, int t) {
   const int sidx = 1 - t;
   Side& S = c->s[sidx];
@@ -361,6 +431,7 @@ int half_sweep(als_ctx* c, int t) {
   double eig_ms = 0.0;
   bool force_heavy = c->p.light_max_degree == 0;
   HIPCHK(hipEventRecord(ev[0], st));
+  if (c->p.nonnegative) return half_sweep_nnls(c, t);
   if (c->p.implicit_prefs) {
     HIPCHK(launch_gram(KP, S.d_X.as<float>(), S.own_n, c->slab.as<double>(), c->slab_blocks, c->d_G.as<double>(), st));
     TRYC(allreduce_G(c));
@@ -574,8 +645,6 @@ int als_create(const als_params* p, als_ctx** out) {
   if (!p || !out) return fail(ALS_E_INVALID_ARGUMENT, "null argument");
   *out = nullptr;
   TRYC(validate(p));
-  if (p->nonnegative)
-    return fail(ALS_E_UNSUPPORTED, "nonnegative=true (NNLS solver) is not built in this engine version yet");
   return ctx_common(p, out);
 }
 

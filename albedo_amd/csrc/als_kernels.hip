@@ -706,6 +706,176 @@ __global__ __launch_bounds__(256, 4) void solve_heavy_kernel(SolveArgs a) {
   }
 }
 
+// =============================================================================================
+// NNLS rows (nonnegative = true; Spark NNLSSolver -> mllib/optimization/NNLS.scala).  Original basis
+// (no rotation: the constraints are coordinate-wise): A = G + λn I + Σ c y yᵀ built exactly like
+// the heavy rows (same LDS stage + MFMA + packed tiles) plus the G tiles, then Spark's projected
+// gradient with CG acceleration, thread i = coordinate i, fp64 vectors and block reductions.
+// =============================================================================================
+template <int N>
+__device__ __forceinline__ void block_sum(double (&v)[N], double* scr, int& phase) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+    for (int o = 32; o > 0; o >>= 1) v[n] += __shfl_xor(v[n], o);
+  double* sp = scr + phase * 32;
+  if (lane == 0) {
+#pragma unroll
+    for (int n = 0; n < N; ++n) sp[wave * 8 + n] = v[n];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int n = 0; n < N; ++n) v[n] = ((sp[n] + sp[8 + n]) + sp[16 + n]) + sp[24 + n];
+  phase ^= 1;
+}
+
+__device__ __forceinline__ double block_min(double v, double* scr, int& phase) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+  double* sp = scr + phase * 32;
+  if (lane == 0) sp[wave * 8] = v;
+  __syncthreads();
+  v = fmin(fmin(sp[0], sp[8]), fmin(sp[16], sp[24]));
+  phase ^= 1;
+  return v;
+}
+
+// (A v)_i for the symmetric matrix held as packed lower tiles; vec in LDS (fp64)
+template <int KP>
+__device__ __forceinline__ double sym_gemv_row(const float* smem, const double* vec, int i) {
+  const int I = i >> 4, ii = i & 15;
+  double acc = 0.0;
+  for (int J = 0; J < I; ++J) {  // row i, tiles left of the diagonal
+    const float* r = smem + htile(I, J) + ii * HT_LD;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) acc += (double)r[c] * vec[16 * J + c];
+  }
+  {
+    const float* t = smem + htile(I, I);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) acc += (double)(c <= ii ? t[ii * HT_LD + c] : t[c * HT_LD + ii]) * vec[16 * I + c];
+  }
+  for (int J = I + 1; J < KP / 16; ++J) {  // column i of the tiles below the diagonal
+    const float* t = smem + htile(J, I) + ii;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) acc += (double)t[c * HT_LD] * vec[16 * J + c];
+  }
+  return acc;
+}
+
+template <int KP>
+struct NnlsLds {
+  static constexpr int BASE = HeavyLds<KP>::FLOATS;       // heavy layout first (tiles, b', flags)
+  static constexpr int OFF_V = (BASE + 1) & ~1;            // fp64 vectors: x, grad, dir (KP each)
+  static constexpr int OFF_SCR = OFF_V + 2 * 3 * KP;       // fp64 reduction scratch [2][4][8]
+  static constexpr int FLOATS = OFF_SCR + 2 * 64;
+};
+
+__device__ __forceinline__ bool nnls_stop(double step, double ndir, double nx) {
+  return isnan(step) || step < 1e-7 || step > 1e40 || ndir < 1e-12 * nx || ndir < 1e-32;
+}
+
+template <int KP>
+__global__ __launch_bounds__(256) void solve_nnls_kernel(SolveArgs a, const float* __restrict__ Gt) {
+  using Lay = HeavyLds<KP>;
+  using NL = NnlsLds<KP>;
+  constexpr int NTL = Lay::NTL;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* bvec = smem + Lay::OFF_B;
+  int* s_flag = reinterpret_cast<int*>(smem + Lay::OFF_FLAG);
+  double* vx = reinterpret_cast<double*>(smem + NL::OFF_V);
+  double* vg = vx + KP;
+  double* vd = vg + KP;
+  double* scr = reinterpret_cast<double*>(smem + NL::OFF_SCR);
+  const int tid = threadIdx.x, wave = tid >> 6;
+  const int j = a.rows[blockIdx.x];
+  const int64_t p0 = a.ptr[j];
+  const int d = (int)(a.ptr[j + 1] - p0);
+  if (tid == 0) s_flag[1] = 0;
+  if (wave == 0) heavy_build<KP, 0>(a, p0, d, smem);
+  else if (wave == 1) heavy_build<KP, 1>(a, p0, d, smem);
+  else if (wave == 2) heavy_build<KP, 2>(a, p0, d, smem);
+  else heavy_build<KP, 3>(a, p0, d, smem);
+  __syncthreads();
+  const float lamn = a.reg * (float)s_flag[0];
+  for (int e = tid; e < NTL * HT_SZ; e += 256) smem[e] += Gt[e];   // A = G + Σ c y yᵀ
+  __syncthreads();
+  for (int c = tid; c < KP; c += 256) smem[hel(c, c)] += c < a.kreal ? lamn : 1.0f;
+  const bool own = tid < KP;
+  const int i = own ? tid : 0;
+  const double bi = own ? (double)bvec[i] : 0.0;
+  double xi = 0.0, last_dir = 0.0, last_norm = 0.0;
+  if (own) vx[i] = 0.0;
+  __syncthreads();
+  int phase = 0, last_wall = 0;
+  const int iter_max = 400 > 20 * a.kreal ? 400 : 20 * a.kreal;
+  for (int iterno = 0; iterno < iter_max; ++iterno) {
+    // residual = A x - b ; projected gradient
+    const double res = own ? sym_gemv_row<KP>(smem, vx, i) - bi : 0.0;
+    double gi = res;
+    if (gi > 0.0 && xi == 0.0) gi = 0.0;
+    if (own) vg[i] = gi;
+    __syncthreads();
+    const double agi = own ? sym_gemv_row<KP>(smem, vg, i) : 0.0;
+    double r1[4] = {gi * gi, gi * res, gi * agi, xi * xi};
+    block_sum<4>(r1, scr, phase);
+    const double ngrad = r1[0], nx = r1[3];
+    double step = r1[1] / (r1[2] + 1e-20);
+    double di = gi, ndir;
+    if (iterno > last_wall + 1) {
+      const double alpha = ngrad / last_norm;
+      di = gi + alpha * last_dir;
+      if (own) vd[i] = di;
+      __syncthreads();
+      const double adi = own ? sym_gemv_row<KP>(smem, vd, i) : 0.0;
+      double r2[3] = {di * res, di * adi, di * di};
+      block_sum<3>(r2, scr, phase);
+      const double dstep = r2[0] / (r2[1] + 1e-20);
+      ndir = r2[2];
+      if (nnls_stop(dstep, ndir, nx)) {
+        di = gi;
+        ndir = ngrad;
+      } else {
+        step = dstep;
+      }
+    } else {
+      ndir = ngrad;
+    }
+    if (nnls_stop(step, ndir, nx)) break;
+    // don't run through the walls: step = min(step, x_i / d_i over d_i > 0 with step d_i > x_i)
+    const double cand = (own && step * di > xi) ? xi / di : INFINITY;
+    step = fmin(step, block_min(cand, scr, phase));
+    // take the step
+    double hit = 0.0;
+    if (own) {
+      if (step * di > xi * (1 - 1e-14)) {
+        xi = 0.0;
+        hit = 1.0;
+      } else {
+        xi -= step * di;
+      }
+      vx[i] = xi;
+    }
+    double r3[1] = {hit};
+    block_sum<1>(r3, scr, phase);
+    if (r3[0] > 0.0) last_wall = iterno;
+    last_dir = di;
+    last_norm = ngrad;
+  }
+  if (own) a.X[(int64_t)j * KP + i] = i < a.kreal ? (float)xi : 0.f;
+  if (tid == 0 && s_flag[1]) atomicOr(a.err, s_flag[1]);
+}
+
+hipError_t launch_solve_nnls(int KP, const SolveArgs& a, const float* Gt, hipStream_t s) {
+  if (a.n_rows <= 0) return hipSuccess;
+  if (KP == 64) solve_nnls_kernel<64><<<(int)a.n_rows, 256, NnlsLds<64>::FLOATS * 4, s>>>(a, Gt);
+  else if (KP == 128) solve_nnls_kernel<128><<<(int)a.n_rows, 256, NnlsLds<128>::FLOATS * 4, s>>>(a, Gt);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+int nnls_gtile_floats(int KP) { const int nb = KP / 16; return nb * (nb + 1) / 2 * HT_SZ; }
+int nnls_gtile_index(int r, int c) { return (r >> 4) * ((r >> 4) + 1) / 2 * HT_SZ + (c >> 4) * HT_SZ + (r & 15) * HT_LD + (c & 15); }
+
 hipError_t launch_solve_heavy(int KP, const SolveArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;
   if (KP == 64) solve_heavy_kernel<64><<<(int)a.n_rows, 256, HeavyLds<64>::FLOATS * 4, s>>>(a);

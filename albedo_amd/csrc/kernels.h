@@ -38,6 +38,11 @@ hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64
 hipError_t launch_solve_light(int KP, int D, const SolveArgs& a, hipStream_t s);
 hipError_t launch_solve_heavy(int KP, const SolveArgs& a, hipStream_t s);
 
+// nonnegative = true: Spark NNLS per row; Gt = the src Gram in packed lower 16x17 tiles (fp32).
+hipError_t launch_solve_nnls(int KP, const SolveArgs& a, const float* Gt, hipStream_t s);
+int nnls_gtile_floats(int KP);
+int nnls_gtile_index(int r, int c);  // r >= c
+
 // Seeded unit-norm Gaussian rows (global row index row0 + r) for large synthetic runs.
 hipError_t launch_init_random(int KP, int kreal, float* X, int64_t n, uint64_t seed, int64_t row0, hipStream_t s);
 

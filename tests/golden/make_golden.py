@@ -111,7 +111,21 @@ def f7_heavy_row():
     np.savez_compressed(os.path.join(OUT, "f7_heavy_row.npz"), user=user, item=item, rating=r, V0=V0, U=U)
 
 
+def f5_nnls():
+    d = generate(SynthSpec(700, 220, 7000, seed=17))
+    B = O.make_blocks(d["user"], d["item"], d["rating"])
+    k = 16
+    U0 = np.abs(init(len(B.user_ids), k, 7))
+    V0 = np.abs(init(len(B.item_ids), k, 8))
+    V1 = O.half_sweep(U0, B.i_ptr, B.i_col, B.i_val, reg=0.5, alpha=40.0, implicit=True, nonnegative=True)
+    U, V = O.fit(B, rank=k, max_iter=2, reg=0.5, alpha=40.0, implicit=True, nonnegative=True,
+                 init_user=U0, init_item=V0)
+    np.savez_compressed(os.path.join(OUT, "f5_nnls.npz"), user=d["user"], item=d["item"], rating=d["rating"],
+                        U0=U0, V0=V0, V1=V1, U=U, V=V)
+
+
 if __name__ == "__main__":
+    f5_nnls()
     f1_half_sweep()
     f2_three_sweeps()
     f3_explicit()

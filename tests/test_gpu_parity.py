@@ -403,3 +403,47 @@ def test_c2_scale_rows_match_fp64_solve(gpu_lib):
         assert np.max(np.abs(U[r] - x)) / np.max(np.abs(x)) < 1e-4
         checked += 1
     assert checked == 200
+
+
+# ---- NNLS (nonnegative = true) --------------------------------------------------------------
+
+def test_golden_f5_nnls_half_sweep_and_fit(gpu_lib):
+    from albedo_amd import _lib as L
+    f = _g("f5_nnls.npz")
+    B = O.make_blocks(f["user"], f["item"], f["rating"])
+    c = Ctx(gpu_lib, 16)
+    # nonnegative context
+    p = L.als_params()
+    L.check(gpu_lib.als_params_default(C.byref(p)))
+    p.rank, p.implicit_prefs, p.reg_param, p.alpha, p.nonnegative, p.max_iter = 16, 1, 0.5, 40.0, 1, 2
+    h = C.c_void_p()
+    L.check(gpu_lib.als_create(C.byref(p), C.byref(h)))
+    c.h = h
+    c.ratings(f["user"], f["item"], f["rating"])
+    c.inject(0, B.user_ids, f["U0"])
+    c.inject(1, B.item_ids, f["V0"])
+    c.half(1)
+    V1 = c.factors(1)[1]
+    assert np.all(V1 >= 0)
+    assert _rel(V1, f["V1"]) < 1e-3
+    zeros_ref = f["V1"] == 0
+    assert np.mean((V1 == 0) == zeros_ref) > 0.995  # same active set up to fp32 ties
+    c.inject(1, B.item_ids, f["V0"])
+    c.L.check(gpu_lib.als_fit(c.h))
+    assert _rel(c.factors(0)[1], f["U"]) < 1e-3 and _rel(c.factors(1)[1], f["V"]) < 1e-3
+
+
+def test_nnls_facade_rank50(gpu_lib):
+    from albedo_amd import ALS
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(500, 160, 6000, seed=36))
+    B = O.make_blocks(d["user"], d["item"], d["rating"])
+    rng = np.random.default_rng(9)
+    U0 = np.abs(rng.standard_normal((len(B.user_ids), 50))).astype(np.float32)
+    V0 = np.abs(rng.standard_normal((len(B.item_ids), 50))).astype(np.float32)
+    model = ALS(rank=50, maxIter=1, implicitPrefs=True, regParam=0.5, alpha=40.0, nonnegative=True).fit(
+        d, initialUserFactors=(B.user_ids, U0), initialItemFactors=(B.item_ids, V0))
+    U, V = O.fit(B, rank=50, max_iter=1, reg=0.5, alpha=40.0, nonnegative=True, init_user=U0, init_item=V0)
+    assert np.all(model.user_factors_np()[1] >= 0)
+    assert _rel(model.item_factors_np()[1], V) < 1e-3
+    assert _rel(model.user_factors_np()[1], U) < 1e-3
