@@ -208,6 +208,7 @@ def cpu_baseline(lib, L, h, k, nnz, n_users, n_items, budget_s):
         order = rng.permutation(n_dst)
         ptr, cols, vals = [0], [], []
         n_row = np.empty(1, np.int64)
+        buf_i, buf_v = np.empty(1 << 16, np.int32), np.empty(1 << 16, np.float32)
         total = 0
         t_rows = 0.0
         done = 0
@@ -217,12 +218,13 @@ def cpu_baseline(lib, L, h, k, nnz, n_users, n_items, budget_s):
             done += len(sel)
             ptr, cols, vals = [0], [], []
             for r in sel:
-                cap = 1 << 22
-                buf_i = np.empty(cap, np.int32)
-                buf_v = np.empty(cap, np.float32)
-                L.check(lib.als_get_row_ratings(h, dst, int(dids[r]), cap, L.ptr(buf_i, C.c_int32),
+                L.check(lib.als_get_row_ratings(h, dst, int(dids[r]), buf_i.size, L.ptr(buf_i, C.c_int32),
                                                 L.ptr(buf_v, C.c_float), L.ptr(n_row, C.c_int64)))
                 m = int(n_row[0])
+                if m > buf_i.size:  # row larger than the buffer: grow once and fetch again
+                    buf_i, buf_v = np.empty(m, np.int32), np.empty(m, np.float32)
+                    L.check(lib.als_get_row_ratings(h, dst, int(dids[r]), m, L.ptr(buf_i, C.c_int32),
+                                                    L.ptr(buf_v, C.c_float), L.ptr(n_row, C.c_int64)))
                 cols.append(np.searchsorted(sids, buf_i[:m]).astype(np.int32))
                 vals.append(buf_v[:m].copy())
                 ptr.append(ptr[-1] + m)
