@@ -92,6 +92,7 @@ struct Side {
   DevBuf d_rows;                 // own local rows grouped by bucket
   int64_t boff[NBUCKET + 1] = {0};
   int64_t bnnz[NBUCKET] = {0};
+  float vmax = 0.f;              // max |rating| over own dst rows (heavy-build fp16 scaling)
   DevBuf d_X;                    // [own_n][KP] factors in basis B
   DevBuf d_Z;                    // [world*maxrows][KP] rotated factors (src role)
   std::vector<double> B;         // [KP][KP] basis: original = X · Bᵀ
@@ -120,7 +121,7 @@ struct als_ctx {
   int64_t nnz = 0;
   bool has_ratings = false;
   bool model_only = false;
-  DevBuf slab, d_G, d_P, d_lam, d_err, d_Gt;
+  DevBuf slab, d_G, d_P, d_lam, d_err, d_Gt, d_cs, d_csmax;
   int slab_blocks = 0;
   hipEvent_t ev[8] = {};
 };
@@ -145,7 +146,7 @@ int validate(const als_params* p) {
   if (p->num_user_blocks < 1) return bad("numUserBlocks", p->num_user_blocks);
   if (p->num_item_blocks < 1) return bad("numItemBlocks", p->num_item_blocks);
   if (padded_rank(p->rank) == 0)
-    return fail(ALS_E_UNSUPPORTED, "rank " + std::to_string(p->rank) + " exceeds the compiled maximum (128)");
+    return fail(ALS_E_UNSUPPORTED, "rank " + std::to_string(p->rank) + " exceeds the compiled maximum (256)");
   return ALS_OK;
 }
 
@@ -312,6 +313,16 @@ int ingest_device(als_ctx* c, int64_t n, const int32_t* d_user, const int32_t* d
   HIPCHK(c->d_P.ensure((size_t)c->KP * c->KP * 4));
   HIPCHK(c->d_lam.ensure((size_t)c->KP * 4));
   HIPCHK(c->d_err.ensure(16));
+  HIPCHK(c->d_cs.ensure((size_t)2 * c->KP * 4));
+  HIPCHK(c->d_csmax.ensure((size_t)c->KP * 4));
+  for (int side = 0; side < 2; ++side) {
+    Side& S = c->s[side];
+    unsigned bits = 0;
+    HIPCHK(launch_absmax(S.d_val.as<float>(), S.own_nnz, c->d_csmax.as<unsigned>(), st));
+    HIPCHK(hipMemcpyAsync(&bits, c->d_csmax.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    std::memcpy(&S.vmax, &bits, 4);
+  }
   c->has_ratings = true;
   return ALS_OK;
 }
@@ -349,6 +360,14 @@ float event_ms(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
+// fp16 column scales of the heavy build for dst side T over the gathered src rows Z
+int column_scales(als_ctx* c, const Side& S, const Side& T) {
+  const float cmax = c->p.implicit_prefs ? (float)c->p.alpha * T.vmax : 1.0f;
+  HIPCHK(launch_colscale(c->KP, S.d_Z.as<float>(), (int64_t)c->world * S.maxrows, cmax, c->d_csmax.as<unsigned>(),
+                         c->d_cs.as<float>(), c->st));
+  return ALS_OK;
+}
+
 // nonnegative = true: Spark's NNLSSolver in the original basis (no rotation; B stays I)
 int half_sweep_nnls(als_ctx* c, int t) {
   const int sidx = 1 - t;
@@ -382,6 +401,7 @@ int half_sweep_nnls(als_ctx* c, int t) {
   TRYC(allgather_rows(c, S.d_Z.as<float>(), S.maxrows));
   HIPCHK(hipEventRecord(ev[4], st));
   HIPCHK(hipMemsetAsync(c->d_err.p, 0, 4, st));
+  TRYC(column_scales(c, S, T));
   HIPCHK(hipEventRecord(ev[5], st));
   SolveArgs a{};
   a.Z = S.d_Z.as<float>();
@@ -395,6 +415,7 @@ int half_sweep_nnls(als_ctx* c, int t) {
   a.alpha = (float)c->p.alpha;
   a.reg = (float)c->p.reg_param;
   a.err = c->d_err.as<int>();
+  a.colscale = c->d_cs.as<float>();
   a.rows = T.d_rows.as<int32_t>();
   a.n_rows = T.boff[NBUCKET];
   HIPCHK(launch_solve_nnls(KP, a, c->d_Gt.as<float>(), st));
@@ -489,6 +510,7 @@ int half_sweep(als_ctx* c, int t) {
   }
   HIPCHK(hipEventRecord(ev[3], st));
   TRYC(allgather_rows(c, S.d_Z.as<float>(), S.maxrows));
+  TRYC(column_scales(c, S, T));
   HIPCHK(hipEventRecord(ev[4], st));
   HIPCHK(hipMemsetAsync(c->d_err.p, 0, 4, st));
   SolveArgs a{};
@@ -503,6 +525,7 @@ int half_sweep(als_ctx* c, int t) {
   a.alpha = (float)c->p.alpha;
   a.reg = (float)c->p.reg_param;
   a.err = c->d_err.as<int>();
+  a.colscale = c->d_cs.as<float>();
   const int32_t* rows = T.d_rows.as<int32_t>();
   static const int Dof[3] = {16, 32, 64};
   T.stats[0] = T.stats[1] = T.stats[2] = T.stats[3] = 0;

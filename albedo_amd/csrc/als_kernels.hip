@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 #include <utility>
 #include "kernels.h"
 
@@ -50,6 +51,14 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+// Dynamic LDS beyond 64 KiB needs the per-kernel attribute (set once per instantiation).
+template <typename K>
+hipError_t allow_lds(K kernel, size_t bytes) {
+  if (bytes <= 65536) return hipSuccess;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)bytes);
+}
+
 struct TilePair { int a, b; };
 // t-th tile of the upper triangle (a <= b) of an nq x nq block grid, row-major.
 __host__ __device__ constexpr TilePair upper_tile(int t, int nq) {
@@ -64,16 +73,20 @@ int padded_rank(int rank) {
   if (rank <= 0) return 0;
   if (rank <= 64) return 64;
   if (rank <= 128) return 128;
+  if (rank <= 256) return 256;
   return 0;
 }
 
 // =============================================================================================
 // Gram: G = Σ_rows x xᵀ  (Spark ALS.computeYtY: NormalEquation.add(y, 0.0) per src row, fp64)
 // =============================================================================================
+template <int KP> constexpr int gram_waves() { return KP >= 256 ? 16 : 4; }  // tile owners per row range
+
 template <int KP, int W>
 __device__ __forceinline__ void gram_body(const float* __restrict__ X, int64_t rb, int64_t re,
                                           double* __restrict__ out) {
-  constexpr int NQ = KP / 16, NT = NQ * (NQ + 1) / 2, NTW = (NT + 3) / 4, NH = KP / 64;
+  constexpr int NWV = gram_waves<KP>();
+  constexpr int NQ = KP / 16, NT = NQ * (NQ + 1) / 2, NTW = (NT + NWV - 1) / NWV, NH = KP / 64;
   const int lane = threadIdx.x & 63, g = lane >> 4, i16 = lane & 15;
   f32x4 acc[NTW];
   double acc64[NTW][4];
@@ -89,7 +102,7 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int64_t r
 #pragma unroll
     for (int h = 0; h < NH; ++h) v[h] = row < re ? ld4(X + row * KP + 64 * h + 4 * i16) : zero4();
     static_for<0, NTW>([&](auto s) {
-      constexpr int t = W + 4 * decltype(s)::value;
+      constexpr int t = W + NWV * decltype(s)::value;
       if constexpr (t < NT) {
         constexpr TilePair p = upper_tile(t, NQ);
         acc[s] = mfma4(v[p.a >> 2][p.a & 3], v[p.b >> 2][p.b & 3], acc[s]);
@@ -106,7 +119,7 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int64_t r
   }
 #pragma unroll
   for (int s = 0; s < NTW; ++s) {
-    const int t = W + 4 * s;
+    const int t = W + NWV * s;
     if (t < NT)
       for (int r = 0; r < 4; ++r) out[((size_t)t * 64 + lane) * 4 + r] = acc64[s][r] + (double)acc[s][r];
   }
@@ -119,11 +132,10 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const float* __restri
   const int64_t rb = (int64_t)blockIdx.x * per_blk;
   const int64_t re = rb + per_blk < n ? rb + per_blk : n;
   double* out = slab + (size_t)blockIdx.x * NT * 256;
-  const int wave = threadIdx.x >> 6;
-  if (wave == 0) gram_body<KP, 0>(X, rb, re, out);
-  else if (wave == 1) gram_body<KP, 1>(X, rb, re, out);
-  else if (wave == 2) gram_body<KP, 2>(X, rb, re, out);
-  else gram_body<KP, 3>(X, rb, re, out);
+  const int wg = blockIdx.y * 4 + (threadIdx.x >> 6);  // blockIdx.y: group of 4 tile owners
+  static_for<0, gram_waves<KP>()>([&](auto w) {
+    if (wg == decltype(w)::value) gram_body<KP, decltype(w)::value>(X, rb, re, out);
+  });
 }
 
 template <int KP>
@@ -162,6 +174,9 @@ hipError_t launch_gram(int KP, const float* X, int64_t n, double* slab, int nblk
   } else if (KP == 128) {
     gram_partial_kernel<128><<<nblk, 256, 0, s>>>(X, n, per, slab);
     gram_reduce_kernel<128><<<(nt * 256 + 255) / 256, 256, 0, s>>>(slab, nblk, G);
+  } else if (KP == 256) {
+    gram_partial_kernel<256><<<dim3(nblk, gram_waves<256>() / 4), 256, 0, s>>>(X, n, per, slab);
+    gram_reduce_kernel<256><<<(nt * 256 + 255) / 256, 256, 0, s>>>(slab, nblk, G);
   } else {
     return hipErrorInvalidValue;
   }
@@ -171,14 +186,17 @@ hipError_t launch_gram(int KP, const float* X, int64_t n, double* slab, int nblk
 // =============================================================================================
 // Rotation: Z = X · M   ([n][KP] x [KP][KP]); M staged in LDS, 64 rows per block iteration.
 // =============================================================================================
+template <int KP> constexpr int rotate_cols() { return KP >= 256 ? 128 : KP; }  // output columns per block
+
 template <int KP>
 __global__ __launch_bounds__(256) void rotate_kernel(const float* __restrict__ X, const float* __restrict__ M,
                                                      float* __restrict__ Z, int64_t n) {
-  constexpr int LDM = KP + 4, NJ = KP / 16;
+  constexpr int NO = rotate_cols<KP>(), LDM = NO + 4, NJ = NO / 16;
   extern __shared__ __attribute__((aligned(16))) float sM[];
-  for (int e = threadIdx.x; e < KP * KP / 4; e += 256) {
-    const int r = (4 * e) / KP, c = (4 * e) % KP;
-    *reinterpret_cast<f32x4*>(sM + r * LDM + c) = ld4(M + r * KP + c);
+  const int co = blockIdx.y * NO;  // this block's output columns co .. co+NO-1
+  for (int e = threadIdx.x; e < KP * NO / 4; e += 256) {
+    const int r = (4 * e) / NO, c = (4 * e) % NO;
+    *reinterpret_cast<f32x4*>(sM + r * LDM + c) = ld4(M + r * KP + co + c);
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
@@ -200,7 +218,7 @@ __global__ __launch_bounds__(256) void rotate_kernel(const float* __restrict__ X
     for (int J = 0; J < NJ; ++J)
       for (int r = 0; r < 4; ++r) {
         const int64_t rr = b * 64 + wave * 16 + 4 * g + r;
-        if (rr < n) Z[rr * KP + 16 * J + i16] = acc[J][r];
+        if (rr < n) Z[rr * KP + co + 16 * J + i16] = acc[J][r];
       }
   }
 }
@@ -209,10 +227,14 @@ hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64
   if (n <= 0) return hipSuccess;
   int64_t blocks = (n + 63) / 64;
   if (blocks > 2048) blocks = 2048;
-  const size_t lds = (size_t)KP * (KP + 4) * sizeof(float);
-  if (KP == 64) rotate_kernel<64><<<(int)blocks, 256, lds, s>>>(X, M, Z, n);
-  else if (KP == 128) rotate_kernel<128><<<(int)blocks, 256, lds, s>>>(X, M, Z, n);
-  else return hipErrorInvalidValue;
+  if (KP == 64) rotate_kernel<64><<<(int)blocks, 256, (size_t)64 * 68 * 4, s>>>(X, M, Z, n);
+  else if (KP == 128) rotate_kernel<128><<<(int)blocks, 256, (size_t)128 * 132 * 4, s>>>(X, M, Z, n);
+  else if (KP == 256) {
+    const size_t lds = (size_t)256 * (rotate_cols<256>() + 4) * 4;
+    static const hipError_t attr = allow_lds(rotate_kernel<256>, lds);
+    if (attr != hipSuccess) return attr;
+    rotate_kernel<256><<<dim3((int)blocks, 256 / rotate_cols<256>()), 256, lds, s>>>(X, M, Z, n);
+  } else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
@@ -263,7 +285,7 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
     vB[I] = __shfl((int)valid, 16 * I + i16) != 0;
   }
   constexpr int NC = KP / 16;
-  constexpr bool KEEPZ = D <= 32;  // keep the gathered rows in registers for the x' epilogue
+  constexpr bool KEEPZ = D <= 32 && D * KP <= 4096;  // keep the gathered rows in registers for x'
   f32x4 zf[KEEPZ ? NB : 1][KEEPZ ? NC : 1];
   if constexpr (KEEPZ) {  // issue every gather up front: one latency for the whole row
 #pragma unroll
@@ -424,148 +446,260 @@ hipError_t launch_solve_light(int KP, int D, const SolveArgs& a, hipStream_t s) 
 #define LIGHT(kp, dd) \
   if (KP == kp && D == dd) { solve_light_kernel<kp, dd><<<blocks, 256, lds, s>>>(a); return hipGetLastError(); }
   LIGHT(64, 16) LIGHT(64, 32) LIGHT(64, 64) LIGHT(128, 16) LIGHT(128, 32) LIGHT(128, 64)
+  LIGHT(256, 16) LIGHT(256, 32) LIGHT(256, 64)
 #undef LIGHT
   return hipErrorInvalidValue;
 }
 
 // =============================================================================================
 // Heavy rows: explicit A' = diag(Λ + λn) + Σ c z zᵀ, b' = Σ w z, then Cholesky + substitutions.
-// One 256-thread workgroup per dst row, sized for 4 workgroups per CU (LDS <= 40 KiB):
-//  build   the row's Z rows are gathered 32 at a time into a double-buffered LDS stage shared by
-//          the 4 waves (one barrier per 32 ratings); each wave owns a fixed set of upper 16x16
-//          tiles (permuted column blocks: one ds_read_b128 per lane per 64 columns) and
-//          accumulates them with v_mfma_f32_16x16x4_f32 on √c-scaled rows (bitwise symmetric).
-//  store   the tiles go to LDS as packed lower-triangular 16x17 tiles (the stage is dead by then).
+// One workgroup per dst row: 4 waves for KP <= 128 (4 workgroups per CU, <= 40 KiB of LDS each),
+// 16 waves for KP = 256 (one workgroup per CU, 150 KiB).
+//  build   the row's Z rows are gathered SPS at a time into registers (double-buffered LDS),
+//          scaled by √c and a per-column power of two (colscale: max |√c z| < 2^13), split into
+//          fp16 hi + lo parts and written COLUMN-major into two LDS images (xor-swizzled 16-B
+//          units, conflict-free fragment reads).  Each wave owns the upper 16x16 tiles of one
+//          pair of column-block groups and accumulates hi·hi + hi·lo + lo·hi with
+//          v_mfma_f32_16x16x32_f16 (32 ratings per MFMA, fp32 accumulation).  The split keeps
+//          22 significant bits and the dropped lo·lo term is 2^-22 relative, i.e. fp32-level
+//          products at 16/3 = 5.3x the fp32-MFMA rate.  b' = Σ w z is accumulated in fp32 from
+//          the raw rows.
+//  store   tiles are unscaled (exact powers of two) into packed lower-triangular 16x17 fp32 tiles
+//          (the stage is dead by then).
 //  factor  right-looking, 16-wide panels, two barriers per panel: the waves that own panel rows
 //          factor the 16x16 diagonal tile redundantly in registers and solve their rows against
-//          it with wave-uniform (SGPR) broadcasts of L11; the trailing update runs on MFMA.  b' is
-//          carried as an extra row, so the forward substitution comes for free.
+//          it with wave-uniform (SGPR) broadcasts of L11; the trailing update runs on fp32 MFMA.
+//          b' is carried as an extra row, so the forward substitution comes for free.
 //  back    Lᵀx = y by one wave, no barriers.
 // =============================================================================================
 constexpr int HT_LD = 17, HT_SZ = 16 * HT_LD;
 __device__ __forceinline__ int htile(int I, int J) { return (I * (I + 1) / 2 + J) * HT_SZ; }
 __device__ __forceinline__ int hel(int r, int c) { return htile(r >> 4, c >> 4) + (r & 15) * HT_LD + (c & 15); }
 
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x4 mfma_h(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
 template <int KP>
-struct HeavyLds {
-  static constexpr int NB = KP / 16, NTL = NB * (NB + 1) / 2;
-  static constexpr int TILES = NTL * HT_SZ, STAGE = 2 * 32 * KP;
+struct Heavy {
+  static constexpr int NW = KP >= 256 ? 16 : 4, NTH = 64 * NW, NQ = KP / 16;
+  static constexpr int SPS = KP >= 256 ? 64 : 32;  // ratings per LDS stage
+  static constexpr int NU = SPS / 8;                // 16-B units per image column row
+  static constexpr int CS = 2 * SPS;                // bytes per image column row
+  static constexpr int IMG = KP * CS;               // bytes per image (4 images: 2 buffers x hi/lo)
+  static constexpr int NCH = KP / 4, NSG = NTH / NCH, NST = SPS / NSG;  // staging map
+  static constexpr bool PERM = KP != 256;           // xor-permuted column order of the image writes
+  static constexpr int SWZ = NU == 4 ? 3 : 5;
+  static constexpr int GS = KP == 64 ? 2 : 4, NG = NQ / GS;  // column-block groups; wave = group pair
+  static constexpr int NTL = NQ * (NQ + 1) / 2;
+  static constexpr int TILES = NTL * HT_SZ, STAGE = IMG;      // floats
   static constexpr int BIG = TILES > STAGE ? TILES : STAGE;
-  static constexpr int OFF_B = BIG, OFF_DIAG = OFF_B + KP, OFF_W = OFF_DIAG + KP, OFF_FLAG = OFF_W + 128;
+  static constexpr int OFF_B = BIG, OFF_DIAG = OFF_B + KP, OFF_FLAG = OFF_DIAG + KP;
   static constexpr int FLOATS = OFF_FLAG + 4;
+  static_assert(NG * NG == NW, "one wave per group pair");
+  static_assert(NSG * NCH == NTH && NST * NSG == SPS && (NST == 2 || NST == 4), "stage map");
+  static_assert(NSG * KP <= STAGE, "b partials fit into the dead stage");
 };
 
-template <int KP, int W>
-__device__ __forceinline__ void heavy_build(const SolveArgs& a, int64_t p0, int d, float* smem) {
-  using Lay = HeavyLds<KP>;
-  constexpr int NQ = KP / 16, NT = NQ * (NQ + 1) / 2, NTW = (NT + 3) / 4, NH = KP / 64;
-  constexpr int F4ROW = KP / 4, RPP = 256 / F4ROW, NPASS = 32 / RPP;
+// byte offset of (column, byte within the column's SPS ratings) in one image
+template <int KP>
+__device__ __forceinline__ int img_off(int col, int byteoff) {
+  using H = Heavy<KP>;
+  const int sw = (col ^ (H::SWZ * (col >> 3))) & (H::NU - 1);
+  return col * H::CS + ((((byteoff >> 4) ^ sw) & (H::NU - 1)) << 4) + (byteoff & 15);
+}
+
+__device__ __forceinline__ uint32_t pack_h2(float a, float b) {
+  f16x2 h = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(uint32_t, h);
+}
+
+// Build of the row's A' tiles owned by this wave: row blocks rb .. rb+NR-1, column blocks
+// cb .. cb+GS-1 (DIAG: the same blocks, upper tiles only).
+template <int KP, bool DIAG>
+__device__ __forceinline__ void heavy_build(const SolveArgs& a, int64_t p0, int d, float* smem, int rb, int cb) {
+  using H = Heavy<KP>;
+  constexpr int NR = DIAG ? H::GS : H::GS / 2, NC = H::GS, NST = H::NST;
+  constexpr int MT = DIAG ? NR * (NR + 1) / 2 : NR * NC;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i16 = lane & 15;
-  float* stage = smem;
-  float* sw = smem + Lay::OFF_W;  // [buf][0..31] = sqrt(c), [buf][32..63] = w
-  const int prow = tid / F4ROW, pch = (tid % F4ROW) * 4;
-  f32x4 acc[NTW];
-#pragma unroll
-  for (int s = 0; s < NTW; ++s) acc[s] = zero4();
-  f32x4 bacc[NH];
-#pragma unroll
-  for (int h = 0; h < NH; ++h) bacc[h] = zero4();
+  char* lds = reinterpret_cast<char*>(smem);
+  int* s_flag = reinterpret_cast<int*>(smem + H::OFF_FLAG);
+  const int cc = tid % H::NCH, sg = tid / H::NCH;
+  const int xr = H::PERM ? (cc & 3) : 0;
+  const f32x4 csc = ld4(a.colscale + 4 * cc);
+  f32x4 bp = zero4();
   int npos = 0;
-  f32x4 stg[NPASS];
-  float wsc = 0.f, ww = 0.f;
+  f32x4 zr[NST];
+  float sq[NST], wv[NST];
+  // loads are unconditional (index clamped to the row's last rating, d >= 1); ratings past the
+  // end get zero weight, so they add nothing to A' or b'
   auto gload = [&](int e0) {
-    int cix[NPASS];
+    int ci[NST];
+    float rv[NST];
+    bool in[NST];
 #pragma unroll
-    for (int p = 0; p < NPASS; ++p) {
-      const int e = e0 + p * RPP + prow;
-      cix[p] = e < d ? a.col[p0 + e] : -1;
+    for (int m = 0; m < NST; ++m) {
+      const int e = e0 + sg * NST + m;
+      in[m] = e < d;
+      const int64_t pe = p0 + (in[m] ? e : d - 1);
+      ci[m] = a.col[pe];
+      rv[m] = a.val[pe];
     }
 #pragma unroll
-    for (int p = 0; p < NPASS; ++p) stg[p] = cix[p] >= 0 ? ld4(a.Z + (int64_t)cix[p] * KP + pch) : zero4();
-    if (tid < 32) {
-      const int e = e0 + tid;
-      float r = 0.f, c = 0.f, w = 0.f;
-      if (e < d) {
-        r = a.val[p0 + e];
-        rating_weights(r, a.implicit, a.alpha, c, w);
-        npos += r > 0.f ? 1 : 0;
-      }
-      wsc = sqrtf(c);
-      ww = w;
+    for (int m = 0; m < NST; ++m) zr[m] = ld4(a.Z + (int64_t)ci[m] * KP + 4 * cc);
+#pragma unroll
+    for (int m = 0; m < NST; ++m) {
+      float c = 0.f, w = 0.f;
+      rating_weights(rv[m], a.implicit, a.alpha, c, w);
+      sq[m] = in[m] ? sqrtf(c) : 0.f;
+      wv[m] = in[m] ? w : 0.f;
+      npos += (cc == 0 && in[m] && rv[m] > 0.f) ? 1 : 0;
     }
   };
+  using PW = typename std::conditional<NST == 4, u32x2, uint32_t>::type;  // NST halves of one column
   auto lds_put = [&](int buf) {
+    char* himg = lds + (2 * buf) * H::IMG;
+    char* limg = himg + H::IMG;
 #pragma unroll
-    for (int p = 0; p < NPASS; ++p)
-      *reinterpret_cast<f32x4*>(stage + (buf * 32 + p * RPP + prow) * KP + pch) = stg[p];
-    if (tid < 32) {
-      sw[buf * 64 + tid] = wsc;
-      sw[buf * 64 + 32 + tid] = ww;
+    for (int m = 0; m < NST; ++m) bp += zr[m] * wv[m];
+    PW hp0, hp1, hp2, hp3, lp0, lp1, lp2, lp3;
+    static_for<0, 4>([&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      PW hv, lv;
+      static_for<0, NST / 2>([&](auto mc) {
+        constexpr int m2 = decltype(mc)::value;
+        float v0 = zr[2 * m2][q] * (sq[2 * m2] * csc[q]);
+        float v1 = zr[2 * m2 + 1][q] * (sq[2 * m2 + 1] * csc[q]);
+        // v is rounded to fp32 ONCE and both hi and lo derive from that register: left alone, the
+        // compiler folds fp16(a·b) into v_fma_mix (rounding the exact product) for lo's hi while
+        // the stored hi rounds the fp32 product; the two disagree at fp16 ties (lo then misses
+        // one fp16 ulp of hi, a 2^-11 error on that element)
+        asm("" : "+v"(v0), "+v"(v1));
+        const _Float16 h0 = (_Float16)v0, h1 = (_Float16)v1;
+        const uint32_t hw = pack_h2(h0, h1), lw = pack_h2(v0 - (float)h0, v1 - (float)h1);
+        if constexpr (NST == 4) { hv[m2] = hw; lv[m2] = lw; } else { hv = hw; lv = lw; }
+      });
+      if constexpr (q == 0) { hp0 = hv; lp0 = lv; }
+      if constexpr (q == 1) { hp1 = hv; lp1 = lv; }
+      if constexpr (q == 2) { hp2 = hv; lp2 = lv; }
+      if constexpr (q == 3) { hp3 = hv; lp3 = lv; }
+    });
+    if constexpr (H::PERM) {  // slot i holds column 4cc + (i ^ xr): spreads the banks of the writes
+      const bool b0 = xr & 1, b1 = xr & 2;
+      const PW h0 = b0 ? hp1 : hp0, h1 = b0 ? hp0 : hp1, h2 = b0 ? hp3 : hp2, h3 = b0 ? hp2 : hp3;
+      const PW l0 = b0 ? lp1 : lp0, l1 = b0 ? lp0 : lp1, l2 = b0 ? lp3 : lp2, l3 = b0 ? lp2 : lp3;
+      hp0 = b1 ? h2 : h0; hp1 = b1 ? h3 : h1; hp2 = b1 ? h0 : h2; hp3 = b1 ? h1 : h3;
+      lp0 = b1 ? l2 : l0; lp1 = b1 ? l3 : l1; lp2 = b1 ? l0 : l2; lp3 = b1 ? l1 : l3;
     }
+    const int boff = 2 * NST * sg;
+    *reinterpret_cast<PW*>(himg + img_off<KP>(4 * cc + (0 ^ xr), boff)) = hp0;
+    *reinterpret_cast<PW*>(limg + img_off<KP>(4 * cc + (0 ^ xr), boff)) = lp0;
+    *reinterpret_cast<PW*>(himg + img_off<KP>(4 * cc + (1 ^ xr), boff)) = hp1;
+    *reinterpret_cast<PW*>(limg + img_off<KP>(4 * cc + (1 ^ xr), boff)) = lp1;
+    *reinterpret_cast<PW*>(himg + img_off<KP>(4 * cc + (2 ^ xr), boff)) = hp2;
+    *reinterpret_cast<PW*>(limg + img_off<KP>(4 * cc + (2 ^ xr), boff)) = lp2;
+    *reinterpret_cast<PW*>(himg + img_off<KP>(4 * cc + (3 ^ xr), boff)) = hp3;
+    *reinterpret_cast<PW*>(limg + img_off<KP>(4 * cc + (3 ^ xr), boff)) = lp3;
   };
+  f32x4 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = zero4();
   gload(0);
   lds_put(0);
   __syncthreads();
-  const int nst = (d + 31) / 32;
+  const int nst = (d + H::SPS - 1) / H::SPS;
   for (int st = 0; st < nst; ++st) {
     const int buf = st & 1;
-    if (st + 1 < nst) gload((st + 1) * 32);
-    const float* sb = stage + buf * 32 * KP;
-#pragma unroll 2
-    for (int q = 0; q < 8; ++q) {
-      const int row = 4 * q + g;
-      const float sc = sw[buf * 64 + row];
-      f32x4 zs[NH];
+    if (st + 1 < nst) gload((st + 1) * H::SPS);
+    const char* himg = lds + (2 * buf) * H::IMG;
+    const char* limg = himg + H::IMG;
 #pragma unroll
-      for (int h = 0; h < NH; ++h) {
-        const f32x4 zv = *reinterpret_cast<const f32x4*>(sb + row * KP + 64 * h + 4 * i16);
-        zs[h] = zv * sc;
-        if (W == 0) bacc[h] += zv * sw[buf * 64 + 32 + row];
+    for (int ks = 0; ks < H::SPS / 32; ++ks) {
+      f16x8 rh[NR], rl[NR];
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const int off = img_off<KP>(16 * (rb + i) + i16, 64 * ks + 16 * g);
+        rh[i] = *reinterpret_cast<const f16x8*>(himg + off);
+        rl[i] = *reinterpret_cast<const f16x8*>(limg + off);
       }
-      static_for<0, NTW>([&](auto s) {
-        constexpr int t = W + 4 * decltype(s)::value;
-        if constexpr (t < NT) {
-          constexpr TilePair p = upper_tile(t, NQ);
-          acc[s] = mfma4(zs[p.a >> 2][p.a & 3], zs[p.b >> 2][p.b & 3], acc[s]);
+      if constexpr (DIAG) {  // column blocks = row blocks
+        int t = 0;
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+#pragma unroll
+          for (int j = i; j < NC; ++j, ++t) {
+            acc[t] = mfma_h(rh[i], rh[j], acc[t]);
+            acc[t] = mfma_h(rh[i], rl[j], acc[t]);
+            acc[t] = mfma_h(rl[i], rh[j], acc[t]);
+          }
+      } else {  // one column block at a time (register pressure)
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          const int off = img_off<KP>(16 * (cb + j) + i16, 64 * ks + 16 * g);
+          const f16x8 ch = *reinterpret_cast<const f16x8*>(himg + off);
+          const f16x8 cl = *reinterpret_cast<const f16x8*>(limg + off);
+#pragma unroll
+          for (int i = 0; i < NR; ++i) {
+            const int t = i * NC + j;
+            acc[t] = mfma_h(rh[i], ch, acc[t]);
+            acc[t] = mfma_h(rh[i], cl, acc[t]);
+            acc[t] = mfma_h(rl[i], ch, acc[t]);
+          }
         }
-      });
+      }
     }
     if (st + 1 < nst) lds_put(buf ^ 1);
     __syncthreads();
   }
-  // stage is dead: store the lower triangle into packed tiles, b' into its vector
-  static_for<0, NTW>([&](auto s) {
-    constexpr int t = W + 4 * decltype(s)::value;
-    if constexpr (t < NT) {
-      constexpr TilePair p = upper_tile(t, NQ);
+  // b' partials into the dead stage, reduced in a fixed order by the first KP threads
+  *reinterpret_cast<f32x4*>(smem + sg * KP + 4 * cc) = bp;
+  if (npos) atomicAdd(&s_flag[0], npos);
+  __syncthreads();
+  if (tid < KP) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < H::NSG; ++q) s += smem[q * KP + tid];
+    smem[H::OFF_B + tid] = s;
+  }
+  __syncthreads();
+  // tiles -> packed lower LDS tiles, unscaled (powers of two: exact)
+  const float* isc = a.colscale + KP;
+  int t = 0;
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const f32x4 ir = ld4(isc + 16 * (rb + i) + 4 * g);
+#pragma unroll
+    for (int j = DIAG ? i : 0; j < NC; ++j, ++t) {
+      const float ic = isc[16 * (cb + j) + i16];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int i = 4 * g + r, jj = i16;
-        if (p.a != p.b || i >= jj) {
-          const int c1 = pcol(p.a, i), c2 = pcol(p.b, jj);
-          smem[c1 > c2 ? hel(c1, c2) : hel(c2, c1)] = acc[s][r];
-        }
+        const int c1 = 16 * (rb + i) + 4 * g + r, c2 = 16 * (cb + j) + i16;
+        if (!DIAG || i != j || c1 >= c2) smem[c1 >= c2 ? hel(c1, c2) : hel(c2, c1)] = acc[t][r] * ir[r] * ic;
       }
     }
-  });
-  if (W == 0) {
-#pragma unroll
-    for (int h = 0; h < NH; ++h)
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        bacc[h][m] += __shfl_xor(bacc[h][m], 16);
-        bacc[h][m] += __shfl_xor(bacc[h][m], 32);
-      }
-    if (lane < 16) {
-#pragma unroll
-      for (int h = 0; h < NH; ++h)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) smem[Lay::OFF_B + 64 * h + 4 * lane + m] = bacc[h][m];
-    }
-    // npos lives in lanes 0..31 of wave 0
-    for (int o = 16; o > 0; o >>= 1) npos += __shfl_xor(npos, o);
-    if (lane == 0) reinterpret_cast<int*>(smem + Lay::OFF_FLAG)[0] = a.implicit ? npos : d;
   }
+}
+
+// Dispatch of the build over the waves: waves 0..NG-1 own the diagonal group pairs, the rest
+// split each off-diagonal group pair (gi < gj) into two halves of its row blocks.
+template <int KP>
+__device__ __forceinline__ void heavy_build_all(const SolveArgs& a, int64_t p0, int d, float* smem) {
+  using H = Heavy<KP>;
+  const int wave = threadIdx.x >> 6;
+  if (wave < H::NG) {
+    heavy_build<KP, true>(a, p0, d, smem, wave * H::GS, wave * H::GS);
+  } else {
+    const int idx = wave - H::NG, pair = idx >> 1, half = idx & 1;
+    int gi = 0, gj = 1;
+    for (int p = 0; p < pair; ++p)
+      if (++gj == H::NG) { ++gi; gj = gi + 1; }
+    heavy_build<KP, false>(a, p0, d, smem, gi * H::GS + half * (H::GS / 2), gj * H::GS);
+  }
+  __syncthreads();
 }
 
 // 16x16 Cholesky of the diagonal tile in registers (lane i16 = row i16).  dg = 1/L[i16][i16].
@@ -590,25 +724,21 @@ __device__ __forceinline__ bool chol16(float (&rr)[16], float& dg, int i) {
 }
 
 template <int KP>
-__global__ __launch_bounds__(256, 4) void solve_heavy_kernel(SolveArgs a) {
-  using Lay = HeavyLds<KP>;
-  constexpr int NB = KP / 16;
+__global__ __launch_bounds__(Heavy<KP>::NTH, 4) void solve_heavy_kernel(SolveArgs a) {
+  using H = Heavy<KP>;
+  constexpr int NB = KP / 16, NTH = H::NTH, NW = H::NW;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* bvec = smem + Lay::OFF_B;
-  float* sdiag = smem + Lay::OFF_DIAG;
-  int* s_flag = reinterpret_cast<int*>(smem + Lay::OFF_FLAG);  // [0] npos, [1] error bits
+  float* bvec = smem + H::OFF_B;
+  float* sdiag = smem + H::OFF_DIAG;
+  int* s_flag = reinterpret_cast<int*>(smem + H::OFF_FLAG);  // [0] npos, [1] error bits
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, i16 = lane & 15;
   const int j = a.rows[blockIdx.x];
   const int64_t p0 = a.ptr[j];
   const int d = (int)(a.ptr[j + 1] - p0);
-  if (tid == 0) s_flag[1] = 0;
-  if (wave == 0) heavy_build<KP, 0>(a, p0, d, smem);
-  else if (wave == 1) heavy_build<KP, 1>(a, p0, d, smem);
-  else if (wave == 2) heavy_build<KP, 2>(a, p0, d, smem);
-  else heavy_build<KP, 3>(a, p0, d, smem);
-  __syncthreads();
-  const float lamn = a.reg * (float)s_flag[0];
-  for (int c = tid; c < KP; c += 256) smem[hel(c, c)] += c < a.kreal ? a.lam[c] + lamn : 1.0f;
+  if (tid == 0) { s_flag[0] = 0; s_flag[1] = 0; }
+  heavy_build_all<KP>(a, p0, d, smem);
+  const float lamn = a.reg * (float)(a.implicit ? s_flag[0] : d);
+  for (int c = tid; c < KP; c += NTH) smem[hel(c, c)] += c < a.kreal ? a.lam[c] + lamn : 1.0f;
   __syncthreads();
   for (int jb = 0; jb < NB; ++jb) {
     const int j0 = 16 * jb;
@@ -647,7 +777,7 @@ __global__ __launch_bounds__(256, 4) void solve_heavy_kernel(SolveArgs a) {
     }
     const int nrem = NB - jb - 1;
     const int ntr = nrem * (nrem + 1) / 2;
-    for (int t = wave; t < ntr; t += 4) {
+    for (int t = wave; t < ntr; t += NW) {
       int ti = 0, tt = t;  // lower tiles (I >= M), row-major
       while (tt > ti) { tt -= ti + 1; ++ti; }
       const int I = jb + 1 + ti, M = jb + 1 + tt;
@@ -662,7 +792,7 @@ __global__ __launch_bounds__(256, 4) void solve_heavy_kernel(SolveArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) ct[(4 * g + r) * HT_LD + i16] = acc[r];
     }
-    for (int m = j0 + 16 + tid; m < KP; m += 256) {
+    for (int m = j0 + 16 + tid; m < KP; m += NTH) {
       float s = bvec[m];
       const float* lr = smem + htile(m >> 4, jb) + (m & 15) * HT_LD;
 #pragma unroll
@@ -712,30 +842,36 @@ __global__ __launch_bounds__(256, 4) void solve_heavy_kernel(SolveArgs a) {
 // the heavy rows (same LDS stage + MFMA + packed tiles) plus the G tiles, then Spark's projected
 // gradient with CG acceleration, thread i = coordinate i, fp64 vectors and block reductions.
 // =============================================================================================
-template <int N>
+template <int NW, int N>
 __device__ __forceinline__ void block_sum(double (&v)[N], double* scr, int& phase) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int n = 0; n < N; ++n)
     for (int o = 32; o > 0; o >>= 1) v[n] += __shfl_xor(v[n], o);
-  double* sp = scr + phase * 32;
+  double* sp = scr + phase * NW * 8;
   if (lane == 0) {
 #pragma unroll
     for (int n = 0; n < N; ++n) sp[wave * 8 + n] = v[n];
   }
   __syncthreads();
 #pragma unroll
-  for (int n = 0; n < N; ++n) v[n] = ((sp[n] + sp[8 + n]) + sp[16 + n]) + sp[24 + n];
+  for (int n = 0; n < N; ++n) {
+    double s = sp[n];
+    for (int w = 1; w < NW; ++w) s += sp[8 * w + n];
+    v[n] = s;
+  }
   phase ^= 1;
 }
 
+template <int NW>
 __device__ __forceinline__ double block_min(double v, double* scr, int& phase) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
-  double* sp = scr + phase * 32;
+  double* sp = scr + phase * NW * 8;
   if (lane == 0) sp[wave * 8] = v;
   __syncthreads();
-  v = fmin(fmin(sp[0], sp[8]), fmin(sp[16], sp[24]));
+  v = sp[0];
+  for (int w = 1; w < NW; ++w) v = fmin(v, sp[8 * w]);
   phase ^= 1;
   return v;
 }
@@ -765,10 +901,11 @@ __device__ __forceinline__ double sym_gemv_row(const float* smem, const double* 
 
 template <int KP>
 struct NnlsLds {
-  static constexpr int BASE = HeavyLds<KP>::FLOATS;       // heavy layout first (tiles, b', flags)
+  static constexpr int NW = Heavy<KP>::NW;
+  static constexpr int BASE = Heavy<KP>::FLOATS;           // heavy layout first (tiles, b', flags)
   static constexpr int OFF_V = (BASE + 1) & ~1;            // fp64 vectors: x, grad, dir (KP each)
-  static constexpr int OFF_SCR = OFF_V + 2 * 3 * KP;       // fp64 reduction scratch [2][4][8]
-  static constexpr int FLOATS = OFF_SCR + 2 * 64;
+  static constexpr int OFF_SCR = OFF_V + 2 * 3 * KP;       // fp64 reduction scratch [2][NW][8]
+  static constexpr int FLOATS = OFF_SCR + 2 * 2 * NW * 8;
 };
 
 __device__ __forceinline__ bool nnls_stop(double step, double ndir, double nx) {
@@ -776,31 +913,27 @@ __device__ __forceinline__ bool nnls_stop(double step, double ndir, double nx) {
 }
 
 template <int KP>
-__global__ __launch_bounds__(256) void solve_nnls_kernel(SolveArgs a, const float* __restrict__ Gt) {
-  using Lay = HeavyLds<KP>;
+__global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a, const float* __restrict__ Gt) {
+  using H = Heavy<KP>;
   using NL = NnlsLds<KP>;
-  constexpr int NTL = Lay::NTL;
+  constexpr int NTL = H::NTL, NTH = H::NTH, NW = H::NW;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* bvec = smem + Lay::OFF_B;
-  int* s_flag = reinterpret_cast<int*>(smem + Lay::OFF_FLAG);
+  float* bvec = smem + H::OFF_B;
+  int* s_flag = reinterpret_cast<int*>(smem + H::OFF_FLAG);
   double* vx = reinterpret_cast<double*>(smem + NL::OFF_V);
   double* vg = vx + KP;
   double* vd = vg + KP;
   double* scr = reinterpret_cast<double*>(smem + NL::OFF_SCR);
-  const int tid = threadIdx.x, wave = tid >> 6;
+  const int tid = threadIdx.x;
   const int j = a.rows[blockIdx.x];
   const int64_t p0 = a.ptr[j];
   const int d = (int)(a.ptr[j + 1] - p0);
-  if (tid == 0) s_flag[1] = 0;
-  if (wave == 0) heavy_build<KP, 0>(a, p0, d, smem);
-  else if (wave == 1) heavy_build<KP, 1>(a, p0, d, smem);
-  else if (wave == 2) heavy_build<KP, 2>(a, p0, d, smem);
-  else heavy_build<KP, 3>(a, p0, d, smem);
+  if (tid == 0) { s_flag[0] = 0; s_flag[1] = 0; }
+  heavy_build_all<KP>(a, p0, d, smem);
+  const float lamn = a.reg * (float)(a.implicit ? s_flag[0] : d);
+  for (int e = tid; e < NTL * HT_SZ; e += NTH) smem[e] += Gt[e];   // A = G + Σ c y yᵀ
   __syncthreads();
-  const float lamn = a.reg * (float)s_flag[0];
-  for (int e = tid; e < NTL * HT_SZ; e += 256) smem[e] += Gt[e];   // A = G + Σ c y yᵀ
-  __syncthreads();
-  for (int c = tid; c < KP; c += 256) smem[hel(c, c)] += c < a.kreal ? lamn : 1.0f;
+  for (int c = tid; c < KP; c += NTH) smem[hel(c, c)] += c < a.kreal ? lamn : 1.0f;
   const bool own = tid < KP;
   const int i = own ? tid : 0;
   const double bi = own ? (double)bvec[i] : 0.0;
@@ -818,7 +951,7 @@ __global__ __launch_bounds__(256) void solve_nnls_kernel(SolveArgs a, const floa
     __syncthreads();
     const double agi = own ? sym_gemv_row<KP>(smem, vg, i) : 0.0;
     double r1[4] = {gi * gi, gi * res, gi * agi, xi * xi};
-    block_sum<4>(r1, scr, phase);
+    block_sum<NW, 4>(r1, scr, phase);
     const double ngrad = r1[0], nx = r1[3];
     double step = r1[1] / (r1[2] + 1e-20);
     double di = gi, ndir;
@@ -829,7 +962,7 @@ __global__ __launch_bounds__(256) void solve_nnls_kernel(SolveArgs a, const floa
       __syncthreads();
       const double adi = own ? sym_gemv_row<KP>(smem, vd, i) : 0.0;
       double r2[3] = {di * res, di * adi, di * di};
-      block_sum<3>(r2, scr, phase);
+      block_sum<NW, 3>(r2, scr, phase);
       const double dstep = r2[0] / (r2[1] + 1e-20);
       ndir = r2[2];
       if (nnls_stop(dstep, ndir, nx)) {
@@ -844,7 +977,7 @@ __global__ __launch_bounds__(256) void solve_nnls_kernel(SolveArgs a, const floa
     if (nnls_stop(step, ndir, nx)) break;
     // don't run through the walls: step = min(step, x_i / d_i over d_i > 0 with step d_i > x_i)
     const double cand = (own && step * di > xi) ? xi / di : INFINITY;
-    step = fmin(step, block_min(cand, scr, phase));
+    step = fmin(step, block_min<NW>(cand, scr, phase));
     // take the step
     double hit = 0.0;
     if (own) {
@@ -857,7 +990,7 @@ __global__ __launch_bounds__(256) void solve_nnls_kernel(SolveArgs a, const floa
       vx[i] = xi;
     }
     double r3[1] = {hit};
-    block_sum<1>(r3, scr, phase);
+    block_sum<NW, 1>(r3, scr, phase);
     if (r3[0] > 0.0) last_wall = iterno;
     last_dir = di;
     last_norm = ngrad;
@@ -866,21 +999,130 @@ __global__ __launch_bounds__(256) void solve_nnls_kernel(SolveArgs a, const floa
   if (tid == 0 && s_flag[1]) atomicOr(a.err, s_flag[1]);
 }
 
+template <int KP>
+hipError_t launch_nnls_kp(const SolveArgs& a, const float* Gt, hipStream_t s) {
+  const size_t lds = NnlsLds<KP>::FLOATS * 4;
+  static const hipError_t attr = allow_lds(solve_nnls_kernel<KP>, lds);
+  if (attr != hipSuccess) return attr;
+  solve_nnls_kernel<KP><<<(int)a.n_rows, Heavy<KP>::NTH, lds, s>>>(a, Gt);
+  return hipGetLastError();
+}
+
 hipError_t launch_solve_nnls(int KP, const SolveArgs& a, const float* Gt, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;
-  if (KP == 64) solve_nnls_kernel<64><<<(int)a.n_rows, 256, NnlsLds<64>::FLOATS * 4, s>>>(a, Gt);
-  else if (KP == 128) solve_nnls_kernel<128><<<(int)a.n_rows, 256, NnlsLds<128>::FLOATS * 4, s>>>(a, Gt);
-  else return hipErrorInvalidValue;
-  return hipGetLastError();
+  if (KP == 64) return launch_nnls_kp<64>(a, Gt, s);
+  if (KP == 128) return launch_nnls_kp<128>(a, Gt, s);
+  if (KP == 256) return launch_nnls_kp<256>(a, Gt, s);
+  return hipErrorInvalidValue;
 }
 int nnls_gtile_floats(int KP) { const int nb = KP / 16; return nb * (nb + 1) / 2 * HT_SZ; }
 int nnls_gtile_index(int r, int c) { return (r >> 4) * ((r >> 4) + 1) / 2 * HT_SZ + (c >> 4) * HT_SZ + (r & 15) * HT_LD + (c & 15); }
 
+template <int KP>
+hipError_t launch_heavy_kp(const SolveArgs& a, hipStream_t s) {
+  const size_t lds = Heavy<KP>::FLOATS * 4;
+  static const hipError_t attr = allow_lds(solve_heavy_kernel<KP>, lds);
+  if (attr != hipSuccess) return attr;
+  solve_heavy_kernel<KP><<<(int)a.n_rows, Heavy<KP>::NTH, lds, s>>>(a);
+  return hipGetLastError();
+}
+
 hipError_t launch_solve_heavy(int KP, const SolveArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;
-  if (KP == 64) solve_heavy_kernel<64><<<(int)a.n_rows, 256, HeavyLds<64>::FLOATS * 4, s>>>(a);
-  else if (KP == 128) solve_heavy_kernel<128><<<(int)a.n_rows, 256, HeavyLds<128>::FLOATS * 4, s>>>(a);
-  else return hipErrorInvalidValue;
+  if (KP == 64) return launch_heavy_kp<64>(a, s);
+  if (KP == 128) return launch_heavy_kp<128>(a, s);
+  if (KP == 256) return launch_heavy_kp<256>(a, s);
+  return hipErrorInvalidValue;
+}
+
+// =============================================================================================
+// Per-column fp16 scales of the heavy build: colscale[c] = 2^e with max_rows |Z[.][c]|·√cmax < 2^13
+// (cmax = the largest confidence c of the dst side), colscale[KP + c] = 2^-e.
+// =============================================================================================
+template <int KP>
+__global__ __launch_bounds__(256) void colmax_kernel(const float* __restrict__ Z, int64_t n, unsigned* __restrict__ out) {
+  constexpr int NCQ = KP / 4, RS = 256 / NCQ;  // float4 column chunks per row, rows per block step
+  __shared__ f32x4 red[256];
+  const int cq = threadIdx.x % NCQ, rsub = threadIdx.x / NCQ;
+  f32x4 m = zero4();
+  int64_t r = (int64_t)blockIdx.x * RS + rsub;
+  const int64_t step = (int64_t)gridDim.x * RS;
+  for (; r + 3 * step < n; r += 4 * step) {  // four independent loads in flight
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ld4(Z + (r + u * step) * KP + 4 * cq);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) m[q] = fmaxf(m[q], fabsf(v[u][q]));
+  }
+  for (; r < n; r += step) {
+    const f32x4 v = ld4(Z + r * KP + 4 * cq);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) m[q] = fmaxf(m[q], fabsf(v[q]));
+  }
+  red[threadIdx.x] = m;
+  __syncthreads();
+  if (threadIdx.x < NCQ) {
+    for (int s = 1; s < RS; ++s) {
+      const f32x4 o = red[s * NCQ + threadIdx.x];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) m[q] = fmaxf(m[q], o[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v = m[q];
+      if (!(v <= 3.0e38f)) v = 3.0e38f;  // NaN / inf: saturate (the solve reports the non-finite result)
+      atomicMax(out + 4 * threadIdx.x + q, __float_as_uint(v));
+    }
+  }
+}
+
+__global__ void colscale_kernel(const unsigned* __restrict__ cmaxbits, int KP, float csqrt, float* __restrict__ out) {
+  const int c = threadIdx.x;
+  if (c >= KP) return;
+  const float m = __uint_as_float(cmaxbits[c]) * csqrt;
+  int e = 0;
+  if (m > 0.f && m <= 3.0e38f) {
+    int ex;
+    frexpf(m, &ex);  // m < 2^ex
+    e = 13 - ex;
+    e = e < -60 ? -60 : (e > 60 ? 60 : e);
+  }
+  out[c] = ldexpf(1.f, e);
+  out[KP + c] = ldexpf(1.f, -e);
+}
+
+__global__ void absmax_kernel(const float* __restrict__ v, int64_t n, unsigned* __restrict__ out) {
+  float m = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(v[i]));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+hipError_t launch_colscale(int KP, const float* Z, int64_t n, float cmax, unsigned* tmp, float* colscale,
+                           hipStream_t s) {
+  hipError_t e = hipMemsetAsync(tmp, 0, KP * sizeof(unsigned), s);
+  if (e != hipSuccess) return e;
+  if (n > 0) {
+    int64_t blocks = (n + 63) / 64;
+    if (blocks > 1024) blocks = 1024;
+    if (KP == 64) colmax_kernel<64><<<(int)blocks, 256, 0, s>>>(Z, n, tmp);
+    else if (KP == 128) colmax_kernel<128><<<(int)blocks, 256, 0, s>>>(Z, n, tmp);
+    else if (KP == 256) colmax_kernel<256><<<(int)blocks, 256, 0, s>>>(Z, n, tmp);
+    else return hipErrorInvalidValue;
+  }
+  colscale_kernel<<<1, KP, 0, s>>>(tmp, KP, sqrtf(cmax > 0.f ? cmax : 1.f), colscale);
+  return hipGetLastError();
+}
+
+hipError_t launch_absmax(const float* v, int64_t n, unsigned* out, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(out, 0, sizeof(unsigned), s);
+  if (e != hipSuccess || n <= 0) return e;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  absmax_kernel<<<(int)blocks, 256, 0, s>>>(v, n, out);
   return hipGetLastError();
 }
 
@@ -1203,6 +1445,9 @@ hipError_t launch_topk(int KP, const TopkArgs& a, hipStream_t s) {
   } else if (KP == 128) {
     topk_kernel<128><<<blocks, 256, lds, s>>>(a);
     topk_rescore_kernel<128><<<(int)((a.n_src + 3) / 4), 256, 0, s>>>(a);
+  } else if (KP == 256) {
+    topk_kernel<256><<<blocks, 256, lds, s>>>(a);
+    topk_rescore_kernel<256><<<(int)((a.n_src + 3) / 4), 256, 0, s>>>(a);
   } else {
     return hipErrorInvalidValue;
   }
@@ -1213,6 +1458,7 @@ hipError_t launch_topk_exact(int KP, const TopkArgs& a, const int32_t* rows, int
   if (n_rows <= 0) return hipSuccess;
   if (KP == 64) topk_exact_kernel<64><<<(int)n_rows, 256, 0, s>>>(a, rows);
   else if (KP == 128) topk_exact_kernel<128><<<(int)n_rows, 256, 0, s>>>(a, rows);
+  else if (KP == 256) topk_exact_kernel<256><<<(int)n_rows, 256, 0, s>>>(a, rows);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

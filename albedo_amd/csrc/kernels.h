@@ -7,7 +7,7 @@
 namespace albedo {
 
 // Padded rank used on device: factor rows are KP floats (zero beyond `rank`).
-int padded_rank(int rank);  // 64 or 128 (0 if unsupported)
+int padded_rank(int rank);  // 64, 128 or 256 (0 if unsupported)
 
 struct SolveArgs {
   const float* Z;          // src factors in the eigenbasis of the src Gram, [*][KP]
@@ -23,6 +23,7 @@ struct SolveArgs {
   float alpha;
   float reg;
   int* err;                // device flag: set to 1 when a solve meets a non-positive pivot
+  const float* colscale;   // [2*KP] heavy-build fp16 column scales 2^e and their inverses
 };
 
 // G (fp64 [KP][KP], full symmetric) = Σ_rows Xᵀ X over rows [0, n) of X ([n][KP]).
@@ -41,6 +42,11 @@ hipError_t launch_solve_heavy(int KP, const SolveArgs& a, hipStream_t s);
 // nonnegative = true: Spark NNLS per row; Gt = the src Gram in packed lower 16x17 tiles (fp32).
 hipError_t launch_solve_nnls(int KP, const SolveArgs& a, const float* Gt, hipStream_t s);
 int nnls_gtile_floats(int KP);
+// colscale[c] = 2^e_c with max_rows |Z[.][c]|·√cmax < 2^13, colscale[KP+c] = 2^-e_c (tmp: KP uints)
+hipError_t launch_colscale(int KP, const float* Z, int64_t n, float cmax, unsigned* tmp, float* colscale,
+                           hipStream_t s);
+// *out = bits of max |v[i]| (non-negative float, compared as unsigned)
+hipError_t launch_absmax(const float* v, int64_t n, unsigned* out, hipStream_t s);
 int nnls_gtile_index(int r, int c);  // r >= c
 
 // Seeded unit-norm Gaussian rows (global row index row0 + r) for large synthetic runs.

@@ -125,7 +125,8 @@ def test_golden_f1_half_sweep_and_gram(gpu_lib, k):
             assert st[0] == 0
 
 
-@pytest.mark.parametrize("k,light", [(50, -1), (50, 0), (64, -1), (100, -1), (128, 0), (128, -1)])
+@pytest.mark.parametrize("k,light", [(50, -1), (50, 0), (64, -1), (100, -1), (128, 0), (128, -1), (200, -1),
+                                     (256, 0), (256, -1)])
 def test_half_sweep_ranks_and_paths(gpu_lib, k, light):
     from albedo_amd.synthetic import SynthSpec, generate
     d = generate(SynthSpec(1500, 600, 30000, seed=20 + k))
@@ -145,6 +146,27 @@ def test_half_sweep_ranks_and_paths(gpu_lib, k, light):
     U_ref = O.half_sweep(V, B.u_ptr, B.u_col, B.u_val, reg=0.5, alpha=40.0)
     _, U = c.factors(0)
     assert _row_rel(U, U_ref) < 1e-4
+
+
+@pytest.mark.parametrize("k", [64, 128, 256])
+def test_heavy_build_column_scaling(gpu_lib, k):
+    """The heavy build splits √c·z into fp16 hi + lo with a per-column power-of-two scale: factor
+    columns spanning 6 decades of magnitude (and one all-zero column) keep the 1e-4 tolerance."""
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(900, 120, 24000, seed=70 + k))
+    B = O.make_blocks(d["user"], d["item"], d["rating"])
+    rng = np.random.default_rng(k + 1)
+    U0 = rng.standard_normal((len(B.user_ids), k)) * np.logspace(-3, 3, k)[None, :]
+    U0[:, k // 3] = 0.0
+    U0 = U0.astype(np.float32)
+    c = Ctx(gpu_lib, k, light=0)  # every row on the heavy (explicit A') path
+    c.ratings(d["user"], d["item"], d["rating"])
+    c.inject(0, B.user_ids, U0)
+    c.inject(1, B.item_ids, np.zeros((len(B.item_ids), k), np.float32))
+    c.half(1)
+    V_ref = O.half_sweep(U0, B.i_ptr, B.i_col, B.i_val, reg=0.5, alpha=40.0)
+    _, V = c.factors(1)
+    assert _row_rel(V, V_ref) < 1e-4
 
 
 def test_golden_f2_three_sweeps_fit(gpu_lib):
@@ -447,3 +469,31 @@ def test_nnls_facade_rank50(gpu_lib):
     assert np.all(model.user_factors_np()[1] >= 0)
     assert _rel(model.item_factors_np()[1], V) < 1e-3
     assert _rel(model.user_factors_np()[1], U) < 1e-3
+
+
+def test_nnls_rank256(gpu_lib):
+    """nonnegative=true at rank 256 (BASELINE config 5's solver and rank), one half-sweep each way."""
+    from albedo_amd import _lib as L
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(160, 60, 2400, seed=41))
+    B = O.make_blocks(d["user"], d["item"], d["rating"])
+    k = 256
+    rng = np.random.default_rng(5)
+    U0 = np.abs(rng.standard_normal((len(B.user_ids), k))).astype(np.float32)
+    U0 /= np.linalg.norm(U0, axis=1, keepdims=True)
+    p = L.als_params()
+    L.check(gpu_lib.als_params_default(C.byref(p)))
+    p.rank, p.implicit_prefs, p.reg_param, p.alpha, p.nonnegative = k, 1, 0.5, 40.0, 1
+    c = Ctx(gpu_lib, 8)
+    h = C.c_void_p()
+    L.check(gpu_lib.als_create(C.byref(p), C.byref(h)))
+    gpu_lib.als_destroy(c.h)
+    c.h, c.rank = h, k
+    c.ratings(d["user"], d["item"], d["rating"])
+    c.inject(0, B.user_ids, U0)
+    c.inject(1, B.item_ids, np.zeros((len(B.item_ids), k), np.float32))
+    c.half(1)
+    V_ref = O.half_sweep(U0, B.i_ptr, B.i_col, B.i_val, reg=0.5, alpha=40.0, nonnegative=True)
+    _, V = c.factors(1)
+    assert np.all(V >= 0)
+    assert _rel(V, V_ref) < 1e-3
