@@ -25,6 +25,14 @@
 
 namespace albedo {
 
+#ifdef ALBEDO_HEAVY_TIMING  // probes only: per-phase clock64 stamps of the first 64 heavy workgroups
+__device__ unsigned long long albedo_heavy_ts[64][48];
+#define HEAVY_TS(k) \
+  if (threadIdx.x == 0 && blockIdx.x < 64) albedo_heavy_ts[blockIdx.x][k] = clock64()
+#else
+#define HEAVY_TS(k)
+#endif
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define WAVE_LDS_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
@@ -536,11 +544,13 @@ __device__ __forceinline__ void heavy_build(const SolveArgs& a, int64_t p0, int 
   f32x4 zr[NST];
   float sq[NST], wv[NST];
   // loads are unconditional (index clamped to the row's last rating, d >= 1); ratings past the
-  // end get zero weight, so they add nothing to A' or b'
-  auto gload = [&](int e0) {
-    int ci[NST];
-    float rv[NST];
-    bool in[NST];
+  // end get zero weight, so they add nothing to A' or b'.  Software pipeline: the (col, val) of
+  // stage st+2 are loaded while the Z rows of stage st+1 are in flight and stage st is on MFMA,
+  // so each stage waits for one HBM latency, not for the dependent index -> row pair.
+  int ci[NST];
+  float rv[NST];
+  bool in[NST];
+  auto iload = [&](int e0) {
 #pragma unroll
     for (int m = 0; m < NST; ++m) {
       const int e = e0 + sg * NST + m;
@@ -549,6 +559,8 @@ __device__ __forceinline__ void heavy_build(const SolveArgs& a, int64_t p0, int 
       ci[m] = a.col[pe];
       rv[m] = a.val[pe];
     }
+  };
+  auto zload = [&]() {
 #pragma unroll
     for (int m = 0; m < NST; ++m) zr[m] = ld4(a.Z + (int64_t)ci[m] * KP + 4 * cc);
 #pragma unroll
@@ -608,13 +620,18 @@ __device__ __forceinline__ void heavy_build(const SolveArgs& a, int64_t p0, int 
   f32x4 acc[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = zero4();
-  gload(0);
+  const int nst = (d + H::SPS - 1) / H::SPS;
+  iload(0);
+  zload();
+  if (nst > 1) iload(H::SPS);
   lds_put(0);
   __syncthreads();
-  const int nst = (d + H::SPS - 1) / H::SPS;
   for (int st = 0; st < nst; ++st) {
     const int buf = st & 1;
-    if (st + 1 < nst) gload((st + 1) * H::SPS);
+    if (st + 1 < nst) {
+      zload();
+      if (st + 2 < nst) iload((st + 2) * H::SPS);
+    }
     const char* himg = lds + (2 * buf) * H::IMG;
     const char* limg = himg + H::IMG;
 #pragma unroll
@@ -702,28 +719,40 @@ __device__ __forceinline__ void heavy_build_all(const SolveArgs& a, int64_t p0, 
   __syncthreads();
 }
 
-// 16x16 Cholesky of the diagonal tile in registers (lane i16 = row i16).  dg = 1/L[i16][i16].
-// A pivot that collapses below 2^-21 of its panel-start value is numerically singular in fp32
-// (Spark's fp64 dppsv reports info > 0 on such systems); it is reported as not positive definite.
-__device__ __forceinline__ bool chol16(float (&rr)[16], float& dg, int i) {
-  bool notpd = false;
-  float dstart[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) dstart[c] = rdlane(rr[c], c);
-#pragma unroll
-  for (int c = 0; c < 16; ++c) {
-    const float piv = rdlane(rr[c], c);
-    if (!(piv > dstart[c] * 4.76837158e-07f)) notpd = true;
-    const float inv = frsq(piv), s = piv * inv;
-    rr[c] = (i == c) ? s : rr[c] * inv;
-    dg = (i == c) ? inv : dg;
-#pragma unroll
-    for (int m = c + 1; m < 16; ++m) rr[m] = fmaf(-rr[c], rdlane(rr[c], m), rr[m]);
-  }
-  return notpd;
+// Broadcast of lane M of every 16-lane row to the whole row (DPP row_newbcast, gfx90a+): the
+// diagonal-block kernels below keep one 16x16 problem per 16-lane row (rows replicated), so a
+// broadcast is one v_mov_dpp instead of a v_readlane + SGPR hazard.
+template <int M>
+__device__ __forceinline__ float bc16(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + M, 0xF, 0xF, true));
 }
 
-template <int KP>
+// 16x16 Cholesky of a diagonal tile in registers: lane i (of each 16-lane row) holds row i (rr[m],
+// m <= i meaningful).  On return rr[m] = L[i][m] (m <= i), dg = 1/L[i][i].  A pivot that collapses
+// below 2^-21 of its start value is numerically singular in fp32 (Spark's fp64 dppsv reports
+// info > 0 on such systems): reported as not positive definite (return value, wave-uniform).
+__device__ __forceinline__ bool chol16(float (&rr)[16], float& dg, int i) {
+  bool notpd = false;
+  float d0 = 0.f;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) d0 = (i == c) ? rr[c] : d0;
+  static_for<0, 16>([&](auto cc) {
+    constexpr int c = decltype(cc)::value;
+    if (i == c && !(rr[c] > d0 * 4.76837158e-07f)) notpd = true;
+    const float piv = bc16<c>(rr[c]);
+    const float inv = frsq(piv), sq = piv * inv;
+    rr[c] = (i == c) ? sq : rr[c] * inv;
+    dg = (i == c) ? inv : dg;
+    static_for<c + 1, 16>([&](auto mm) {
+      constexpr int m = decltype(mm)::value;
+      rr[m] = fmaf(-rr[c], bc16<m>(rr[c]), rr[m]);
+    });
+  });
+  return __any(notpd);
+}
+
+// PH: phase mask for profiling probes (bit 0 build, bit 1 factor + substitution); the engine runs 3.
+template <int KP, int PH = 3>
 __global__ __launch_bounds__(Heavy<KP>::NTH, 4) void solve_heavy_kernel(SolveArgs a) {
   using H = Heavy<KP>;
   constexpr int NB = KP / 16, NTH = H::NTH, NW = H::NW;
@@ -736,92 +765,141 @@ __global__ __launch_bounds__(Heavy<KP>::NTH, 4) void solve_heavy_kernel(SolveArg
   const int64_t p0 = a.ptr[j];
   const int d = (int)(a.ptr[j + 1] - p0);
   if (tid == 0) { s_flag[0] = 0; s_flag[1] = 0; }
-  heavy_build_all<KP>(a, p0, d, smem);
+  HEAVY_TS(0);
+  if constexpr (PH & 1) {
+    heavy_build_all<KP>(a, p0, d, smem);
+  } else {
+    for (int e = tid; e < H::OFF_DIAG; e += NTH) smem[e] = 0.f;
+    __syncthreads();
+  }
+  if constexpr (!(PH & 2)) {
+    for (int c = tid; c < KP; c += NTH) a.X[(int64_t)j * KP + c] = smem[H::OFF_B + c] + smem[hel(c, c)];
+    return;
+  }
+  HEAVY_TS(1);
   const float lamn = a.reg * (float)(a.implicit ? s_flag[0] : d);
   for (int c = tid; c < KP; c += NTH) smem[hel(c, c)] += c < a.kreal ? a.lam[c] + lamn : 1.0f;
   __syncthreads();
-  for (int jb = 0; jb < NB; ++jb) {
-    const int j0 = 16 * jb;
-    const int nrow = KP - j0 - 16 + 1;  // rows below the panel + the b' row
-    float rr[16];
-    float dg = 1.f;
-    bool notpd = false;
-    if (wave * 64 < nrow) {
+  // Blocked right-looking Cholesky, 16-wide panels, look-ahead, two barriers per panel:
+  //  A  all waves: TRSM of the rows below the panel (and b') against L11, broadcast LDS reads
+  //  B  wave 0: update + factor the next diagonal tile (chol16); waves 1..: the rest of the
+  //     trailing update on MFMA and the b' update
+  // Diagonal tiles are re-laid as L11ᵀ in a 16-float row layout (row c = column c of L11, zero
+  // above the diagonal; tile starts are 16-B aligned) for the TRSM and the back substitution.
+  auto diag_factor = [&](int jb) {  // wave 0
+    float* t = smem + htile(jb, jb);
+    float rr[16], dg = 1.f;
 #pragma unroll
-      for (int m = 0; m < 16; ++m) rr[m] = smem[htile(jb, jb) + i16 * HT_LD + m];
-      notpd = chol16(rr, dg, i16);
-      const int ridx = wave * 64 + lane;
-      if (ridx < nrow) {  // L21 row = A21 row · L11⁻ᵀ with L11 broadcast from the registers
+    for (int m = 0; m < 16; ++m) rr[m] = t[i16 * HT_LD + m];
+    const bool np = chol16(rr, dg, i16);
+    WAVE_LDS_SYNC();
+    if (lane < 16) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) t[c * 16 + i16] = c <= i16 ? rr[c] : 0.f;
+      sdiag[16 * jb + i16] = dg;
+    }
+    if (np && lane == 0) s_flag[1] = 2;
+  };
+  // C(I,M) -= L(I,jb) L(M,jb)ᵀ on MFMA (packed lower 16x17 tiles)
+  auto tile_update = [&](int jb, int I, int M) {
+    float* ct = smem + htile(I, M);
+    const float* at = smem + htile(I, jb) + i16 * HT_LD + g;
+    const float* bt = smem + htile(M, jb) + i16 * HT_LD + g;
+    f32x4 acc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = ct[(4 * g + r) * HT_LD + i16];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) acc = mfma4(-at[4 * s4], bt[4 * s4], acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ct[(4 * g + r) * HT_LD + i16] = acc[r];
+  };
+  if (wave == 0) diag_factor(0);
+  __syncthreads();
+  HEAVY_TS(2);
+  for (int jb = 0; jb < NB; ++jb) {
+    const int j0 = 16 * jb, nrem = NB - 1 - jb;
+    // ---- A
+    {
+      const int ridx = tid, nrow = KP - j0 - 16 + 1;  // rows below the panel + the b' row
+      if (ridx < nrow) {
         const int i = j0 + 16 + ridx;
         float* src = i < KP ? smem + htile(i >> 4, jb) + (i & 15) * HT_LD : bvec + j0;
+        const float* lt = smem + htile(jb, jb);
         float x[16];
 #pragma unroll
         for (int m = 0; m < 16; ++m) x[m] = src[m];
+        f32x4 dv[4];
 #pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          x[c] *= rdlane(dg, c);
+        for (int q = 0; q < 4; ++q) dv[q] = ld4(sdiag + j0 + 4 * q);
+        static_for<0, 16>([&](auto cc) {
+          constexpr int c = decltype(cc)::value;
+          x[c] *= dv[c >> 2][c & 3];
+          static_for<(c + 1) / 4, 4>([&](auto qq) {
+            constexpr int q = decltype(qq)::value;
+            const f32x4 l = ld4(lt + 16 * c + 4 * q);
 #pragma unroll
-          for (int m = c + 1; m < 16; ++m) x[m] = fmaf(-x[c], rdlane(rr[c], m), x[m]);
-        }
+            for (int e = 0; e < 4; ++e)
+              if (4 * q + e > c) x[4 * q + e] = fmaf(-x[c], l[e], x[4 * q + e]);
+          });
+          if constexpr ((c & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted loads
+        });
 #pragma unroll
         for (int m = 0; m < 16; ++m) src[m] = x[m];
       }
     }
     __syncthreads();
-    if (wave == 0 && lane < 16) {  // L11 back into its tile (read again only by the back substitution)
+    // ---- B
+    if (wave == 0) {
+      if (nrem > 0) {
+        tile_update(jb, jb + 1, jb + 1);
+        WAVE_LDS_SYNC();
+        diag_factor(jb + 1);
+      }
+    } else if (nrem > 0) {
+      const int ntr = nrem * (nrem + 1) / 2;
+      for (int t = wave; t < ntr; t += NW - 1) {
+        int ti = 0, tt = t;  // lower tiles (I >= M) row-major; t = 0 is the next diagonal tile
+        while (tt > ti) { tt -= ti + 1; ++ti; }
+        tile_update(jb, jb + 1 + ti, jb + 1 + tt);
+      }
+      for (int m = j0 + 16 + tid - 64; m < KP; m += NTH - 64) {
+        float sv = bvec[m];
+        const float* lr = smem + htile(m >> 4, jb) + (m & 15) * HT_LD;
 #pragma unroll
-      for (int m = 0; m < 16; ++m)
-        if (m <= i16) smem[htile(jb, jb) + i16 * HT_LD + m] = rr[m];
-      sdiag[j0 + i16] = dg;
-      if (notpd) s_flag[1] = 2;
-    }
-    const int nrem = NB - jb - 1;
-    const int ntr = nrem * (nrem + 1) / 2;
-    for (int t = wave; t < ntr; t += NW) {
-      int ti = 0, tt = t;  // lower tiles (I >= M), row-major
-      while (tt > ti) { tt -= ti + 1; ++ti; }
-      const int I = jb + 1 + ti, M = jb + 1 + tt;
-      float* ct = smem + htile(I, M);
-      const float* at = smem + htile(I, jb) + i16 * HT_LD + g;
-      const float* bt = smem + htile(M, jb) + i16 * HT_LD + g;
-      f32x4 acc;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = ct[(4 * g + r) * HT_LD + i16];
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) acc = mfma4(-at[4 * s4], bt[4 * s4], acc);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ct[(4 * g + r) * HT_LD + i16] = acc[r];
-    }
-    for (int m = j0 + 16 + tid; m < KP; m += NTH) {
-      float s = bvec[m];
-      const float* lr = smem + htile(m >> 4, jb) + (m & 15) * HT_LD;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) s = fmaf(-bvec[j0 + c], lr[c], s);
-      bvec[m] = s;
+        for (int c = 0; c < 16; ++c) sv = fmaf(-bvec[j0 + c], lr[c], sv);
+        bvec[m] = sv;
+      }
     }
     __syncthreads();
+    HEAVY_TS(3 + jb);
   }
-  if (wave == 0) {  // back substitution Lᵀ x = y, single wave
+  if (wave == 0) {  // back substitution Lᵀ x = y, one wave (lane i16 of every 16-lane row: x[j0+i16])
     for (int jb = NB - 1; jb >= 0; --jb) {
       const int j0 = 16 * jb;
       float yv = bvec[j0 + i16];
       const float sdq = sdiag[j0 + i16];
-      float lcol[16];
+      float lcol[16];  // L11[m][i16] = row i16 of the stored L11ᵀ
 #pragma unroll
-      for (int m = 0; m < 16; ++m) lcol[m] = smem[htile(jb, jb) + m * HT_LD + i16];
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 l = ld4(smem + htile(jb, jb) + 16 * i16 + 4 * q);
 #pragma unroll
-      for (int i = 15; i >= 0; --i) {
-        const float xi = rdlane(yv * sdq, i);
-        yv = (i16 < i) ? fmaf(-lcol[i], xi, yv) : ((i16 == i) ? xi : yv);
+        for (int e = 0; e < 4; ++e) lcol[4 * q + e] = l[e];
       }
-      if (lane < 16) bvec[j0 + i16] = yv;
+      float xb[16];  // x_J[c] on every lane
+      static_for<0, 16>([&](auto cc) {
+        constexpr int i = 15 - decltype(cc)::value;
+        const float xi = bc16<i>(yv * sdq);
+        xb[i] = xi;
+        yv = (i16 < i) ? fmaf(-lcol[i], xi, yv) : ((i16 == i) ? xi : yv);
+      });
       WAVE_LDS_SYNC();
-      for (int m = lane; m < j0; m += 64) {
-        float s = bvec[m];
+      if (lane < 16) bvec[j0 + i16] = yv;
+      for (int m = lane; m < j0; m += 64) {  // y_m -= Σ_c L[j0+c][m] x_J[c]
+        float sv = bvec[m];
         const float* lt = smem + htile(jb, m >> 4) + (m & 15);
 #pragma unroll
-        for (int c = 0; c < 16; ++c) s = fmaf(-lt[c * HT_LD], bvec[j0 + c], s);
-        bvec[m] = s;
+        for (int c = 0; c < 16; ++c) sv = fmaf(-lt[c * HT_LD], xb[c], sv);
+        bvec[m] = sv;
       }
       WAVE_LDS_SYNC();
     }
@@ -833,6 +911,7 @@ __global__ __launch_bounds__(Heavy<KP>::NTH, 4) void solve_heavy_kernel(SolveArg
     }
     if (__any(nonfinite)) s_flag[1] |= 2;
     if (lane == 0 && s_flag[1]) atomicOr(a.err, s_flag[1]);
+    HEAVY_TS(23);
   }
 }
 
