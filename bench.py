@@ -137,13 +137,14 @@ def main():
     d = kern[dom]
     achieved = d["bytes_per_sweep"] / (d["ms"] / 1000.0) / 1e9 if d["ms"] > 0 else 0.0
     peak = 8000.0
+    # HBM bytes of the same kernel from the committed PMC passes of this config (tools/prof.sh ->
+    # tools/traffic.py; rocprof cannot run inside the timed bench): GB per sweep, like bytes_per_sweep
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json")
-    if os.path.exists(tpath):
-        try:
-            traffic = json.load(open(tpath)).get(dom)
-        except Exception:
-            traffic = None
+    if os.path.exists(tpath) and world == 1:
+        entry = json.load(open(tpath)).get(dom)
+        if entry:
+            traffic = entry["hbm_gb_per_sweep"]
 
     # ---- top-30 users/s (secondary metric; a bounded user subset) ------------------------------
     topk_ups = None
@@ -175,6 +176,8 @@ def main():
                        "rank": k, "nnz": int(nnz), "parallelism": f"row-shard x{world} (RCCL)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                          "frac": achieved / peak, "traffic": traffic, "kernel": dom,
+                         "traffic_unit": "GB per sweep (PMC, profiles/pmc_traffic_<config>.json)",
+                         "algorithmic_gb_per_sweep": d["bytes_per_sweep"] / 1e9,
                          "kernel_ms_per_sweep": d["ms"]},
             "cpu_baseline": cpu,
             "topk30_users_per_s": topk_ups,
