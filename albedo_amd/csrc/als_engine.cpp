@@ -920,16 +920,14 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
       pos.push_back(i);
     }
   if (known.empty() || T.n == 0) return ALS_OK;
-  // max dst row norm (error bound of the MFMA pre-selection)
+  // max dst row norm (error bound of the MFMA pre-selection), on the device
   double tmax = 0.0;
   {
-    std::vector<float> h((size_t)T.n * KP);
-    HIPCHK(hipMemcpy(h.data(), T.d_orig.p, h.size() * 4, hipMemcpyDeviceToHost));
-    for (int64_t r = 0; r < T.n; ++r) {
-      double s2 = 0.0;
-      for (int j = 0; j < c->p.rank; ++j) s2 += (double)h[(size_t)r * KP + j] * h[(size_t)r * KP + j];
-      tmax = std::max(tmax, std::sqrt(s2));
-    }
+    DevBuf d_nrm;
+    HIPCHK(d_nrm.ensure(8));
+    HIPCHK(launch_rownorm_max(T.d_orig.as<float>(), T.n, KP, c->p.rank, d_nrm.as<unsigned long long>(), c->st));
+    HIPCHK(hipMemcpyAsync(&tmax, d_nrm.p, 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
   }
   DevBuf d_dstids;
   HIPCHK(d_dstids.ensure(T.n * 4));

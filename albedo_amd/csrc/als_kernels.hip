@@ -1283,7 +1283,6 @@ hipError_t launch_predict(int KP, int kreal, const float* U, const float* V, con
 //          any non-candidate has approx <= t (the KC-th approx score) so exact <= t + e; if the
 //          k-th exact score is not > t + e the row is flagged for an exact full scan.
 // =============================================================================================
-constexpr int TK_CAP = 128;  // per (wave, src row) list capacity
 
 // key order: higher score first, then lower index
 __device__ __forceinline__ bool tk_before(float s1, int i1, float s2, int i2) {
@@ -1338,18 +1337,40 @@ __device__ __forceinline__ void wave_bitonic(float (&sc)[NPL], int (&ix)[NPL]) {
   bitonic_stages<NPL, 2>(sc, ix, threadIdx.x & 63);
 }
 
+// Pass 1: one workgroup per 64 src rows (wave w owns rows 16w .. 16w+15, fragments in registers);
+// dst rows stream through LDS in chunks of NI, the next chunk prefetched into registers while the
+// current one is on MFMA.  Chunk rows are stored with their 16-B units XOR-swizzled by 4·(row&3),
+// so a fragment read (16 rows x 4 consecutive units) spreads evenly over the banks.  Every
+// workgroup walks the dst rows in the same order, so the chunks of an XCD's workgroups are L2 hits.
+// Candidate lists hold CAP entries per src row and are compacted to the best 64 (threshold = the
+// 64th) only when fewer than 64 slots remain, i.e. about once per CAP-64 arrivals: arrivals decay
+// like 64/n over the scan, so a large CAP makes compaction rare.
+template <int KP>
+struct TopkLds {
+  static constexpr int NI = KP == 64 ? 128 : 64, NJ = NI / 16;  // dst rows per LDS chunk (32-64 KB)
+  static constexpr int CAP = KP >= 256 ? 160 : 240;             // list capacity per src row
+  static constexpr int NSORT = 4;                               // sort width per lane (256 slots)
+  static constexpr int CHUNK = NI * KP;                         // floats
+  static constexpr int LISTS = 64 * CAP;                        // (score, idx) per src row
+  static constexpr int FLOATS = CHUNK + 2 * LISTS + 128;        // + counts and thresholds
+  static constexpr int NLD = NI * KP / 4 / 256;                 // float4 per thread per chunk
+  static_assert(CAP <= 64 * NSORT && CAP >= 128 && FLOATS * 4 <= 160 * 1024, "list capacity, LDS");
+};
+__device__ __forceinline__ int tk_unit(int row, int u) { return u ^ (4 * (row & 3)); }
+
 template <int KP>
 __global__ __launch_bounds__(256) void topk_kernel(TopkArgs a) {
-  constexpr int NC = KP / 16;  // 16-column chunks
+  using TL = TopkLds<KP>;
+  constexpr int NC = KP / 16, NI = TL::NI, NJ = TL::NJ, NLD = TL::NLD;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* lsc = smem;                                           // [4][16][CAP]
-  int* lix = reinterpret_cast<int*>(smem + 4 * 16 * TK_CAP);   // [4][16][CAP]
-  int* lcnt = lix + 4 * 16 * TK_CAP;                           // [4][16]
-  float* lthr = reinterpret_cast<float*>(lcnt + 64);           // [4][16]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
-  const int64_t sb = (int64_t)blockIdx.x * 16;
-  if (threadIdx.x < 64) { lcnt[threadIdx.x] = 0; lthr[threadIdx.x] = -INFINITY; }
-  // src fragments: lane holds row (sb + i16), columns c0 + 4g .. +3 for every chunk
+  float* tch = smem;                                             // [NI][KP], swizzled units
+  float* lsc = smem + TL::CHUNK;                                 // [64][CAP]
+  int* lix = reinterpret_cast<int*>(lsc + TL::LISTS);            // [64][CAP]
+  int* lcnt = lix + TL::LISTS;                                   // [64]
+  float* lthr = reinterpret_cast<float*>(lcnt + 64);             // [64]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, i16 = lane & 15;
+  const int64_t sb = (int64_t)blockIdx.x * 64 + 16 * wave;       // this wave's first src row
+  if (tid < 64) { lcnt[tid] = 0; lthr[tid] = -INFINITY; }
   f32x4 su[NC];
   {
     const int64_t si = sb + i16;
@@ -1357,84 +1378,115 @@ __global__ __launch_bounds__(256) void topk_kernel(TopkArgs a) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) su[c] = srow >= 0 ? ld4(a.S + (int64_t)srow * KP + 16 * c + 4 * g) : zero4();
   }
-  __syncthreads();
-  float* wsc = lsc + wave * 16 * TK_CAP;
-  int* wix = lix + wave * 16 * TK_CAP;
+  constexpr int CAP = TL::CAP, NS = TL::NSORT;
+  float* wsc = lsc + wave * 16 * CAP;
+  int* wix = lix + wave * 16 * CAP;
   int* wcnt = lcnt + wave * 16;
   float* wthr = lthr + wave * 16;
-  for (int64_t j0 = (int64_t)wave * 64; j0 < a.n_dst; j0 += 256) {
-    f32x4 acc[4];
+  // chunk loader: element e = tid + 256 u of the chunk's NI*KP/4 float4 (row-major)
+  f32x4 pf[NLD];
+  auto gload = [&](int64_t j0) {
 #pragma unroll
-    for (int J = 0; J < 4; ++J) acc[J] = zero4();
+    for (int u = 0; u < NLD; ++u) {
+      const int e = tid + 256 * u, r = e / (KP / 4), q = e % (KP / 4);
+      const int64_t dj = j0 + r;
+      pf[u] = dj < a.n_dst ? ld4(a.T + dj * KP + 4 * q) : zero4();
+    }
+  };
+  auto lput = [&]() {
+#pragma unroll
+    for (int u = 0; u < NLD; ++u) {
+      const int e = tid + 256 * u, r = e / (KP / 4), q = e % (KP / 4);
+      *reinterpret_cast<f32x4*>(tch + r * KP + 4 * tk_unit(r, q)) = pf[u];
+    }
+  };
+  float thr[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};  // rows 4g + r of this wave
+  gload(0);
+  for (int64_t j0 = 0; j0 < a.n_dst; j0 += NI) {
+    __syncthreads();  // previous chunk consumed
+    lput();
+    __syncthreads();
+    if (j0 + NI < a.n_dst) gload(j0 + NI);
+    f32x4 acc[NJ];
+#pragma unroll
+    for (int J = 0; J < NJ; ++J) acc[J] = zero4();
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      f32x4 tv[4];
+      f32x4 tv[NJ];
 #pragma unroll
-      for (int J = 0; J < 4; ++J) {
-        const int64_t dj = j0 + 16 * J + i16;
-        tv[J] = dj < a.n_dst ? ld4(a.T + dj * KP + 16 * c + 4 * g) : zero4();
+      for (int J = 0; J < NJ; ++J) {
+        const int row = 16 * J + i16;
+        tv[J] = *reinterpret_cast<const f32x4*>(tch + row * KP + 4 * tk_unit(row, 4 * c + g));
       }
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int J = 0; J < 4; ++J) acc[J] = mfma4(su[c][m], tv[J][m], acc[J]);
+        for (int J = 0; J < NJ; ++J) acc[J] = mfma4(su[c][m], tv[J][m], acc[J]);
     }
-    // append candidates: lane holds src rows 4g + r, dst j0 + 16J + i16
+    // append candidates 64 dst rows at a time (a list holds <= 64 kept + 64 new): lane holds src
+    // rows 4g + r (of this wave's 16), dst j0 + 16J + i16; thresholds live in registers
+    static_for<0, NJ / 4>([&](auto hh) {
+      constexpr int h = decltype(hh)::value;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int sr = 4 * g + r;
-      const float thr = wthr[sr];
+      for (int r = 0; r < 4; ++r) {
+        const int sr = 4 * g + r;
 #pragma unroll
-      for (int J = 0; J < 4; ++J) {
-        const int64_t dj = j0 + 16 * J + i16;
-        const float sc = acc[J][r];
-        if (dj < a.n_dst && sc >= thr) {
-          const int pos = atomicAdd(&wcnt[sr], 1);
-          wsc[sr * TK_CAP + pos] = sc;
-          wix[sr * TK_CAP + pos] = (int)dj;
+        for (int J = 4 * h; J < 4 * h + 4; ++J) {
+          const int64_t dj = j0 + 16 * J + i16;
+          const float sc = acc[J][r];
+          if (dj < a.n_dst && sc >= thr[r]) {
+            const int pos = atomicAdd(&wcnt[sr], 1);
+            wsc[sr * CAP + pos] = sc;
+            wix[sr * CAP + pos] = (int)dj;
+          }
         }
       }
-    }
-    WAVE_LDS_SYNC();
-    // compact rows that could overflow on the next tile (each tile adds <= 64 per row)
-    for (int sr = 0; sr < 16; ++sr) {
-      const int cnt = wcnt[sr];
-      if (cnt > TK_CAP - 64) {
-        float s2[2];
-        int i2[2];
+      WAVE_LDS_SYNC();
+      // compact the rows that could overflow on the next 64 (best 64 kept, threshold = the 64th)
+      const int mycnt = lane < 16 ? wcnt[lane] : 0;
+      unsigned long long full = __ballot(mycnt > CAP - 64);
+      if (full) {
+        while (full) {
+          const int sr = __builtin_ctzll(full);
+          full &= full - 1;
+          const int cnt = rdlane_i(mycnt, sr);
+          float s2[NS];
+          int i2[NS];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int e = lane + 64 * h;
-          s2[h] = e < cnt ? wsc[sr * TK_CAP + e] : -INFINITY;
-          i2[h] = e < cnt ? wix[sr * TK_CAP + e] : -1;
+          for (int q = 0; q < NS; ++q) {
+            const int e = lane + 64 * q;
+            s2[q] = e < cnt ? wsc[sr * CAP + e] : -INFINITY;
+            i2[q] = e < cnt ? wix[sr * CAP + e] : -1;
+          }
+          wave_bitonic<NS>(s2, i2);
+          WAVE_LDS_SYNC();
+          wsc[sr * CAP + lane] = s2[0];
+          wix[sr * CAP + lane] = i2[0];
+          if (lane == 63) wthr[sr] = s2[0];
+          if (lane == 0) wcnt[sr] = 64;
+          WAVE_LDS_SYNC();
         }
-        wave_bitonic<2>(s2, i2);
-        WAVE_LDS_SYNC();
-        wsc[sr * TK_CAP + lane] = s2[0];
-        wix[sr * TK_CAP + lane] = i2[0];
-        if (lane == 63) wthr[sr] = s2[0];
-        if (lane == 0) wcnt[sr] = 64;
-        WAVE_LDS_SYNC();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) thr[r] = wthr[4 * g + r];
       }
-    }
+    });
   }
-  __syncthreads();
-  // merge the 4 waves' lists per src row: wave w handles rows w, w+4, w+8, w+12
-  for (int sr = wave; sr < 16; sr += 4) {
+  // each wave owns its rows' lists: best KC per row
+  for (int sr = 0; sr < 16; ++sr) {
     const int64_t si = sb + sr;
     if (si >= a.n_src) break;
-    float s8[8];
-    int i8[8];
+    const int cnt = wcnt[sr];
+    float s2[NS];
+    int i2[NS];
 #pragma unroll
-    for (int h = 0; h < 8; ++h) {
-      const int w = h >> 1, e = lane + 64 * (h & 1);
-      const int cnt = lcnt[w * 16 + sr];
-      s8[h] = e < cnt ? lsc[(w * 16 + sr) * TK_CAP + e] : -INFINITY;
-      i8[h] = e < cnt ? lix[(w * 16 + sr) * TK_CAP + e] : -1;
+    for (int h = 0; h < NS; ++h) {
+      const int e = lane + 64 * h;
+      s2[h] = e < cnt ? wsc[sr * CAP + e] : -INFINITY;
+      i2[h] = e < cnt ? wix[sr * CAP + e] : -1;
     }
-    wave_bitonic<8>(s8, i8);
-    a.cand[si * TOPK_KC + lane] = i8[0];
-    a.cand_score[si * TOPK_KC + lane] = s8[0];
+    wave_bitonic<NS>(s2, i2);
+    a.cand[si * TOPK_KC + lane] = i2[0];
+    a.cand_score[si * TOPK_KC + lane] = s2[0];
   }
 }
 
@@ -1514,22 +1566,44 @@ __global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32
   }
 }
 
+template <int KP>
+hipError_t launch_topk_kp(const TopkArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)TopkLds<KP>::FLOATS * 4;
+  static const hipError_t attr = allow_lds(topk_kernel<KP>, lds);
+  if (attr != hipSuccess) return attr;
+  topk_kernel<KP><<<(int)((a.n_src + 63) / 64), 256, lds, s>>>(a);
+  topk_rescore_kernel<KP><<<(int)((a.n_src + 3) / 4), 256, 0, s>>>(a);
+  return hipGetLastError();
+}
+
 hipError_t launch_topk(int KP, const TopkArgs& a, hipStream_t s) {
   if (a.n_src <= 0) return hipSuccess;
-  const int blocks = (int)((a.n_src + 15) / 16);
-  const size_t lds = (size_t)4 * 16 * TK_CAP * 8 + 128 * 4;
-  if (KP == 64) {
-    topk_kernel<64><<<blocks, 256, lds, s>>>(a);
-    topk_rescore_kernel<64><<<(int)((a.n_src + 3) / 4), 256, 0, s>>>(a);
-  } else if (KP == 128) {
-    topk_kernel<128><<<blocks, 256, lds, s>>>(a);
-    topk_rescore_kernel<128><<<(int)((a.n_src + 3) / 4), 256, 0, s>>>(a);
-  } else if (KP == 256) {
-    topk_kernel<256><<<blocks, 256, lds, s>>>(a);
-    topk_rescore_kernel<256><<<(int)((a.n_src + 3) / 4), 256, 0, s>>>(a);
-  } else {
-    return hipErrorInvalidValue;
+  if (KP == 64) return launch_topk_kp<64>(a, s);
+  if (KP == 128) return launch_topk_kp<128>(a, s);
+  if (KP == 256) return launch_topk_kp<256>(a, s);
+  return hipErrorInvalidValue;
+}
+
+// max_r ||T[r][0..kreal)||_2 (fp64), stored as the bits of a non-negative double
+__global__ void rownorm_max_kernel(const float* __restrict__ T, int64_t n, int KP, int kreal,
+                                   unsigned long long* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  double best = 0.0;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += (int64_t)gridDim.x * 4) {
+    double s2 = 0.0;
+    for (int c = lane; c < kreal; c += 64) s2 += (double)T[r * KP + c] * (double)T[r * KP + c];
+    for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
+    best = fmax(best, s2);
   }
+  if (lane == 0) atomicMax(out, (unsigned long long)__double_as_longlong(sqrt(best)));
+}
+
+hipError_t launch_rownorm_max(const float* T, int64_t n, int KP, int kreal, unsigned long long* out, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(out, 0, 8, s);
+  if (e != hipSuccess || n <= 0) return e;
+  int64_t blocks = (n + 3) / 4;
+  if (blocks > 4096) blocks = 4096;
+  rownorm_max_kernel<<<(int)blocks, 256, 0, s>>>(T, n, KP, kreal, out);
   return hipGetLastError();
 }
 

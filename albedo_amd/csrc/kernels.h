@@ -75,6 +75,8 @@ struct TopkArgs {
 };
 hipError_t launch_topk(int KP, const TopkArgs& a, hipStream_t s);
 hipError_t launch_topk_exact(int KP, const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s);
+// *out = bits of max_r ||T[r][0..kreal)||_2 computed in fp64
+hipError_t launch_rownorm_max(const float* T, int64_t n, int KP, int kreal, unsigned long long* out, hipStream_t s);
 constexpr int TOPK_KC = 64;  // candidates kept per src row by the MFMA pass
 
 // Ingest (ingest.hip): COO -> remap + CSR.
