@@ -44,6 +44,14 @@ __device__ __forceinline__ float rdlane(float x, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
 }
 __device__ __forceinline__ int rdlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+// Broadcast of lane M of every 16-lane row to the whole row (DPP row_newbcast, gfx90a+): the
+// diagonal-block kernels below keep one 16x16 problem per 16-lane row (rows replicated), so a
+// broadcast is one v_mov_dpp instead of a v_readlane + SGPR hazard.
+template <int M>
+__device__ __forceinline__ float bc16(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + M, 0xF, 0xF, true));
+}
+
 // v_rsq_f32 / v_rcp_f32 / v_sqrt_f32: single instructions (~1 ulp) instead of the IEEE-exact
 // multi-instruction expansions; the solve tolerance is 1e-4 relative (tests state it)
 __device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
@@ -353,27 +361,48 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
     const float v = Ks[me * LDK + m];
     kr[m] = (m == me) ? (valid ? v + cinv : 1.0f) : (valid ? v : 0.0f);
   }
-  // Cholesky K = L Lᵀ, lane i holds row i (entries m <= i are L[i][m] when done)
+  // Cholesky K = L Lᵀ, lane i holds row i (entries m <= i are L[i][m] when done); then the forward
+  // substitution L y = C⁻¹ w.  D = 16: broadcasts of lane c by DPP row_newbcast (rows 0..15 sit in
+  // lanes 0..15; the other 16-lane rows broadcast their own unused copies); D > 16: readlane.
   bool notpd = false;
   float dg = 1.f;  // 1 / L[me][me]
+  float y = valid ? we * cinv : 0.f;
+  if constexpr (D == 16) {
+    static_for<0, D>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      const float piv = bc16<c>(kr[c]);
+      if (!(piv > 0.f)) notpd = true;
+      const float inv = frsq(piv), s = piv * inv;
+      kr[c] = (me == c) ? s : kr[c] * inv;
+      dg = (me == c) ? inv : dg;
+      static_for<c + 1, D>([&](auto mm) {
+        constexpr int m = decltype(mm)::value;
+        kr[m] = fmaf(-kr[c], bc16<m>(kr[c]), kr[m]);
+      });
+    });
+    static_for<0, D>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      const float yc = bc16<c>(y * dg);
+      y = (me > c) ? fmaf(-kr[c], yc, y) : ((me == c) ? yc : y);
+    });
+  } else {
 #pragma unroll
-  for (int c = 0; c < D; ++c) {
-    const float piv = rdlane(kr[c], c);
-    if (!(piv > 0.f)) notpd = true;
-    const float inv = frsq(piv), s = piv * inv;
-    kr[c] = (me == c) ? s : kr[c] * inv;
-    dg = (me == c) ? inv : dg;
+    for (int c = 0; c < D; ++c) {
+      const float piv = rdlane(kr[c], c);
+      if (!(piv > 0.f)) notpd = true;
+      const float inv = frsq(piv), s = piv * inv;
+      kr[c] = (me == c) ? s : kr[c] * inv;
+      dg = (me == c) ? inv : dg;
 #pragma unroll
-    for (int m = c + 1; m < D; ++m) kr[m] = fmaf(-kr[c], rdlane(kr[c], m), kr[m]);
+      for (int m = c + 1; m < D; ++m) kr[m] = fmaf(-kr[c], rdlane(kr[c], m), kr[m]);
+    }
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      const float yc = rdlane(y * dg, c);
+      y = (me > c) ? fmaf(-kr[c], yc, y) : ((me == c) ? yc : y);
+    }
   }
   if (notpd && lane == 0) atomicOr(a.err, 2);
-  // forward: L y = C⁻¹ w
-  float y = valid ? we * cinv : 0.f;
-#pragma unroll
-  for (int c = 0; c < D; ++c) {
-    const float yc = rdlane(y * dg, c);
-    y = (me > c) ? fmaf(-kr[c], yc, y) : ((me == c) ? yc : y);
-  }
   // transpose L through LDS: lane i gets column i (lt[m] = L[m][i])
   WAVE_LDS_SYNC();
   if (lane < D) {
@@ -385,10 +414,18 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
 #pragma unroll
   for (int m = 0; m < D; ++m) lt[m] = Ks[m * LDK + me];
   // backward: Lᵀ v = y
+  if constexpr (D == 16) {
+    static_for<0, D>([&](auto cc) {
+      constexpr int c = D - 1 - decltype(cc)::value;
+      const float vc = bc16<c>(y * dg);
+      y = (me < c) ? fmaf(-lt[c], vc, y) : ((me == c) ? vc : y);
+    });
+  } else {
 #pragma unroll
-  for (int c = D - 1; c >= 0; --c) {
-    const float vc = rdlane(y * dg, c);
-    y = (me < c) ? fmaf(-lt[c], vc, y) : ((me == c) ? vc : y);
+    for (int c = D - 1; c >= 0; --c) {
+      const float vc = rdlane(y * dg, c);
+      y = (me < c) ? fmaf(-lt[c], vc, y) : ((me == c) ? vc : y);
+    }
   }
   // x' = D⁻¹ Zᵀ v
   if constexpr (KEEPZ) {
@@ -717,14 +754,6 @@ __device__ __forceinline__ void heavy_build_all(const SolveArgs& a, int64_t p0, 
     heavy_build<KP, false>(a, p0, d, smem, gi * H::GS + half * (H::GS / 2), gj * H::GS);
   }
   __syncthreads();
-}
-
-// Broadcast of lane M of every 16-lane row to the whole row (DPP row_newbcast, gfx90a+): the
-// diagonal-block kernels below keep one 16x16 problem per 16-lane row (rows replicated), so a
-// broadcast is one v_mov_dpp instead of a v_readlane + SGPR hazard.
-template <int M>
-__device__ __forceinline__ float bc16(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + M, 0xF, 0xF, true));
 }
 
 // 16x16 Cholesky of a diagonal tile in registers: lane i (of each 16-lane row) holds row i (rr[m],
