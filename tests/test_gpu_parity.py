@@ -301,6 +301,37 @@ def test_golden_f4_topk_bit_exact_with_ties(gpu_lib, num):
         gpu_lib.als_destroy(h)
 
 
+@pytest.mark.parametrize("rank,num", [(50, 30), (100, 64), (200, 30)])
+def test_topk_large_catalogue_bit_exact(gpu_lib, rank, num):
+    """Top-k over a catalogue of hundreds of LDS chunks (every padded rank: 64, 128, 256), a src count
+    that is not a multiple of the 64-row workgroup tile, and exact score ties (duplicated dst
+    factor rows, tie-break by id) against the F2J-order oracle, ids and score bits."""
+    from albedo_amd import _lib as L
+    rng = np.random.default_rng(rank)
+    n_u, n_i = 333, 30011
+    uid = (np.arange(n_u, dtype=np.int32) * 7 + 11)
+    iid = rng.permutation(np.arange(n_i, dtype=np.int32) * 3 + 5).astype(np.int32)
+    uf = rng.standard_normal((n_u, rank)).astype(np.float32)
+    itf = (rng.standard_normal((n_i, rank)) * rng.uniform(0.2, 1.5, (n_i, 1))).astype(np.float32)
+    itf[n_i // 2: n_i // 2 + 200] = itf[:200]  # exact duplicates: equal scores, different ids
+    h = C.c_void_p()
+    L.check(gpu_lib.als_model_create(rank, n_u, L.ptr(uid, C.c_int32), L.ptr(uf, C.c_float), n_i,
+                                     L.ptr(iid, C.c_int32), L.ptr(itf, C.c_float), -1, C.byref(h)))
+    try:
+        src = np.empty(n_u, np.int32)
+        ids = np.empty((n_u, num), np.int32)
+        sc = np.empty((n_u, num), np.float32)
+        L.check(gpu_lib.als_recommend(h, 0, num, None, n_u, L.ptr(src, C.c_int32), L.ptr(ids, C.c_int32),
+                                      L.ptr(sc, C.c_float)))
+        ref_ids, ref_sc = O.recommend_for_all(uid, uf, iid, itf, num)
+        order = np.argsort(uid)
+        assert np.array_equal(src, uid[order])
+        assert np.array_equal(ids, ref_ids[order])
+        assert np.array_equal(sc.view(np.uint32), ref_sc[order].view(np.uint32))
+    finally:
+        gpu_lib.als_destroy(h)
+
+
 def test_topk_subset_unknown_ids_and_small_catalogue(gpu_lib):
     from albedo_amd import _lib as L
     rng = np.random.default_rng(7)
