@@ -920,15 +920,31 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
       pos.push_back(i);
     }
   if (known.empty() || T.n == 0) return ALS_OK;
-  // max dst row norm (error bound of the MFMA pre-selection), on the device
-  double tmax = 0.0;
+  // max row norms (error bound of the pre-selection; fp16 split scales), on the device
+  double tmax = 0.0, smax = 0.0;
   {
     DevBuf d_nrm;
-    HIPCHK(d_nrm.ensure(8));
+    HIPCHK(d_nrm.ensure(16));
     HIPCHK(launch_rownorm_max(T.d_orig.as<float>(), T.n, KP, c->p.rank, d_nrm.as<unsigned long long>(), c->st));
-    HIPCHK(hipMemcpyAsync(&tmax, d_nrm.p, 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(launch_rownorm_max(S.d_orig.as<float>(), S.n, KP, c->p.rank, d_nrm.as<unsigned long long>() + 1, c->st));
+    double nr[2];
+    HIPCHK(hipMemcpyAsync(nr, d_nrm.p, 16, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
+    tmax = nr[0];
+    smax = nr[1];
   }
+  // |entry| <= row norm, so scaling by 2^(13 - ceil(log2 max norm)) keeps every split value < 2^13
+  auto pow2_scale = [](double m) {
+    if (!(m > 0.0) || !std::isfinite(m)) return 1.0;
+    int e = 0;
+    std::frexp(m, &e);  // m < 2^e
+    e = std::max(-60, std::min(60, 13 - e));
+    return std::ldexp(1.0, e);
+  };
+  const double ssc = pow2_scale(smax), tsc = pow2_scale(tmax);
+  DevBuf d_tsplit;
+  HIPCHK(d_tsplit.ensure((size_t)T.n * KP * 4));
+  HIPCHK(launch_split_rows(T.d_orig.as<float>(), T.n, KP, (float)tsc, d_tsplit.p, c->st));
   DevBuf d_dstids;
   HIPCHK(d_dstids.ensure(T.n * 4));
   HIPCHK(hipMemcpy(d_dstids.p, T.ids.data(), T.n * 4, hipMemcpyHostToDevice));
@@ -954,6 +970,9 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
     a.kreal = c->p.rank;
     a.k = k;
     a.tmax_norm = (float)(tmax * (1.0 + 1e-6));
+    a.Tsplit = d_tsplit.p;
+    a.ssc = (float)ssc;
+    a.unscale = (float)(1.0 / (ssc * tsc));
     a.cand = d_cand.as<int32_t>();
     a.cand_score = d_cs.as<float>();
     a.out_ids = d_oid.as<int32_t>();

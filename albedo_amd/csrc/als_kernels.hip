@@ -1366,33 +1366,60 @@ __device__ __forceinline__ void wave_bitonic(float (&sc)[NPL], int (&ix)[NPL]) {
   bitonic_stages<NPL, 2>(sc, ix, threadIdx.x & 63);
 }
 
-// Pass 1: one workgroup per 64 src rows (wave w owns rows 16w .. 16w+15, fragments in registers);
-// dst rows stream through LDS in chunks of NI, the next chunk prefetched into registers while the
-// current one is on MFMA.  Chunk rows are stored with their 16-B units XOR-swizzled by 4·(row&3),
-// so a fragment read (16 rows x 4 consecutive units) spreads evenly over the banks.  Every
-// workgroup walks the dst rows in the same order, so the chunks of an XCD's workgroups are L2 hits.
+// Pass 1: one workgroup per 64 src rows (wave w owns rows 16w .. 16w+15); scores on split-fp16
+// MFMA: every factor row is scaled by a power of two (max |v| < 2^13) and split into fp16 hi + lo,
+// and hi·hi + hi·lo + lo·hi is accumulated with v_mfma_f32_16x16x32_f16 — products to 2^-22, the
+// same order as fp32 rounding, at 16/3 the fp32-MFMA rate.  The pre-selection only has to keep a
+// superset of the top k: the rescoring pass certifies it with a bound that includes this error.
+// The src fragments live in registers (hi/lo f16x8 per 32 columns); the dst rows (pre-split by
+// split_rows) stream through LDS in chunks of NI, the next chunk prefetched into registers while
+// the current one is on MFMA, rows stored with their 16-B units XOR-swizzled by 4·(row&3) so a
+// fragment read (16 rows x 4 consecutive units) spreads over the banks.  Every workgroup walks
+// the dst rows in the same order, so an XCD's workgroups share the chunks in L2.
 // Candidate lists hold CAP entries per src row and are compacted to the best 64 (threshold = the
-// 64th) only when fewer than 64 slots remain, i.e. about once per CAP-64 arrivals: arrivals decay
-// like 64/n over the scan, so a large CAP makes compaction rare.
+// 64th) only when fewer than 64 slots remain: arrivals decay like 64/n over the scan.
 template <int KP>
 struct TopkLds {
-  static constexpr int NI = KP == 64 ? 128 : 64, NJ = NI / 16;  // dst rows per LDS chunk (32-64 KB)
-  static constexpr int CAP = KP >= 256 ? 160 : 240;             // list capacity per src row
-  static constexpr int NSORT = 4;                               // sort width per lane (256 slots)
-  static constexpr int CHUNK = NI * KP;                         // floats
-  static constexpr int LISTS = 64 * CAP;                        // (score, idx) per src row
-  static constexpr int FLOATS = CHUNK + 2 * LISTS + 128;        // + counts and thresholds
-  static constexpr int NLD = NI * KP / 4 / 256;                 // float4 per thread per chunk
+  static constexpr int NI = KP >= 256 ? 64 : 128, NJ = NI / 16;  // dst rows per LDS chunk
+  static constexpr int RB = 4 * KP;                               // bytes per split dst row
+  static constexpr int CAP = KP >= 256 ? 160 : (KP == 128 ? 176 : 240);  // list capacity per row
+  static constexpr int NSORT = 4;                                 // sort width per lane (256 slots)
+  static constexpr int CHUNK = NI * KP;                           // floats (NI * RB bytes)
+  static constexpr int LISTS = 64 * CAP;                          // (score, idx) per src row
+  static constexpr int FLOATS = CHUNK + 2 * LISTS + 128;          // + counts and thresholds
+  static constexpr int NLD = NI * RB / 16 / 256;                  // 16-B units per thread per chunk
   static_assert(CAP <= 64 * NSORT && CAP >= 128 && FLOATS * 4 <= 160 * 1024, "list capacity, LDS");
 };
 __device__ __forceinline__ int tk_unit(int row, int u) { return u ^ (4 * (row & 3)); }
 
+__global__ void split_rows_kernel(const float* __restrict__ T, int64_t n, int KP, float scale,
+                                  _Float16* __restrict__ out) {
+  const int64_t tot = n * KP;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    float v = T[e] * scale;
+    asm("" : "+v"(v));  // one fp32 rounding, then hi and lo from that value (see lds_put)
+    const _Float16 h = (_Float16)v;
+    const int64_t r = e / KP, c = e % KP;
+    out[r * 2 * KP + c] = h;
+    out[r * 2 * KP + KP + c] = (_Float16)(v - (float)h);
+  }
+}
+
+hipError_t launch_split_rows(const float* T, int64_t n, int KP, float scale, void* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  int64_t blocks = (n * KP + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  split_rows_kernel<<<(int)blocks, 256, 0, s>>>(T, n, KP, scale, reinterpret_cast<_Float16*>(out));
+  return hipGetLastError();
+}
+
 template <int KP>
 __global__ __launch_bounds__(256) void topk_kernel(TopkArgs a) {
   using TL = TopkLds<KP>;
-  constexpr int NC = KP / 16, NI = TL::NI, NJ = TL::NJ, NLD = TL::NLD;
+  constexpr int NQ = KP / 32, NI = TL::NI, NJ = TL::NJ, NLD = TL::NLD, RB = TL::RB;
+  constexpr int CAP = TL::CAP, NS = TL::NSORT, UPR = RB / 16;  // 16-B units per dst row
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* tch = smem;                                             // [NI][KP], swizzled units
+  char* tch = reinterpret_cast<char*>(smem);                     // [NI][RB], swizzled units
   float* lsc = smem + TL::CHUNK;                                 // [64][CAP]
   int* lix = reinterpret_cast<int*>(lsc + TL::LISTS);            // [64][CAP]
   int* lcnt = lix + TL::LISTS;                                   // [64]
@@ -1400,33 +1427,48 @@ __global__ __launch_bounds__(256) void topk_kernel(TopkArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, i16 = lane & 15;
   const int64_t sb = (int64_t)blockIdx.x * 64 + 16 * wave;       // this wave's first src row
   if (tid < 64) { lcnt[tid] = 0; lthr[tid] = -INFINITY; }
-  f32x4 su[NC];
+  // src fragments: lane (i16, g) holds row sb + i16, columns 32q + 8g .. +7, split hi / lo
+  f16x8 uh[NQ], ul[NQ];
   {
     const int64_t si = sb + i16;
     const int srow = si < a.n_src ? a.src_rows[si] : -1;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) su[c] = srow >= 0 ? ld4(a.S + (int64_t)srow * KP + 16 * c + 4 * g) : zero4();
+    for (int q = 0; q < NQ; ++q) {
+      f32x4 v0 = zero4(), v1 = zero4();
+      if (srow >= 0) {
+        v0 = ld4(a.S + (int64_t)srow * KP + 32 * q + 8 * g);
+        v1 = ld4(a.S + (int64_t)srow * KP + 32 * q + 8 * g + 4);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float v = (e < 4 ? v0[e] : v1[e - 4]) * a.ssc;
+        asm("" : "+v"(v));
+        const _Float16 h = (_Float16)v;
+        uh[q][e] = h;
+        ul[q][e] = (_Float16)(v - (float)h);
+      }
+    }
   }
-  constexpr int CAP = TL::CAP, NS = TL::NSORT;
   float* wsc = lsc + wave * 16 * CAP;
   int* wix = lix + wave * 16 * CAP;
   int* wcnt = lcnt + wave * 16;
   float* wthr = lthr + wave * 16;
-  // chunk loader: element e = tid + 256 u of the chunk's NI*KP/4 float4 (row-major)
+  const char* Tb = reinterpret_cast<const char*>(a.Tsplit);
+  // chunk loader: 16-B unit e = tid + 256 u of the chunk (row-major, UPR units per row)
   f32x4 pf[NLD];
   auto gload = [&](int64_t j0) {
 #pragma unroll
     for (int u = 0; u < NLD; ++u) {
-      const int e = tid + 256 * u, r = e / (KP / 4), q = e % (KP / 4);
+      const int e = tid + 256 * u, r = e / UPR, q = e % UPR;
       const int64_t dj = j0 + r;
-      pf[u] = dj < a.n_dst ? ld4(a.T + dj * KP + 4 * q) : zero4();
+      pf[u] = dj < a.n_dst ? *reinterpret_cast<const f32x4*>(Tb + dj * RB + 16 * q) : zero4();
     }
   };
   auto lput = [&]() {
 #pragma unroll
     for (int u = 0; u < NLD; ++u) {
-      const int e = tid + 256 * u, r = e / (KP / 4), q = e % (KP / 4);
-      *reinterpret_cast<f32x4*>(tch + r * KP + 4 * tk_unit(r, q)) = pf[u];
+      const int e = tid + 256 * u, r = e / UPR, q = e % UPR;
+      *reinterpret_cast<f32x4*>(tch + r * RB + 16 * tk_unit(r, q)) = pf[u];
     }
   };
   float thr[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};  // rows 4g + r of this wave
@@ -1440,20 +1482,20 @@ __global__ __launch_bounds__(256) void topk_kernel(TopkArgs a) {
 #pragma unroll
     for (int J = 0; J < NJ; ++J) acc[J] = zero4();
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      f32x4 tv[NJ];
+    for (int q = 0; q < NQ; ++q) {
 #pragma unroll
       for (int J = 0; J < NJ; ++J) {
         const int row = 16 * J + i16;
-        tv[J] = *reinterpret_cast<const f32x4*>(tch + row * KP + 4 * tk_unit(row, 4 * c + g));
+        // hi units 0 .. KP/8-1, lo units KP/8 .. KP/4-1; this lane's 8 columns: unit 4q + g
+        const f16x8 th = *reinterpret_cast<const f16x8*>(tch + row * RB + 16 * tk_unit(row, 4 * q + g));
+        const f16x8 tl = *reinterpret_cast<const f16x8*>(tch + row * RB + 16 * tk_unit(row, KP / 8 + 4 * q + g));
+        acc[J] = mfma_h(uh[q], th, acc[J]);
+        acc[J] = mfma_h(uh[q], tl, acc[J]);
+        acc[J] = mfma_h(ul[q], th, acc[J]);
       }
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int J = 0; J < NJ; ++J) acc[J] = mfma4(su[c][m], tv[J][m], acc[J]);
     }
-    // append candidates 64 dst rows at a time (a list holds <= 64 kept + 64 new): lane holds src
-    // rows 4g + r (of this wave's 16), dst j0 + 16J + i16; thresholds live in registers
+    // append candidates 64 dst rows at a time (a list holds <= CAP-64 kept + 64 new): lane holds
+    // src rows 4g + r (of this wave's 16), dst j0 + 16J + i16; thresholds live in registers
     static_for<0, NJ / 4>([&](auto hh) {
       constexpr int h = decltype(hh)::value;
 #pragma unroll
@@ -1462,7 +1504,7 @@ __global__ __launch_bounds__(256) void topk_kernel(TopkArgs a) {
 #pragma unroll
         for (int J = 4 * h; J < 4 * h + 4; ++J) {
           const int64_t dj = j0 + 16 * J + i16;
-          const float sc = acc[J][r];
+          const float sc = acc[J][r] * a.unscale;
           if (dj < a.n_dst && sc >= thr[r]) {
             const int pos = atomicAdd(&wcnt[sr], 1);
             wsc[sr * CAP + pos] = sc;
@@ -1548,7 +1590,10 @@ __global__ __launch_bounds__(256) void topk_rescore_kernel(TopkArgs a) {
     const double u = 5.9604644775390625e-08;  // 2^-24
     const double kk = (double)(a.kreal + 2);
     const double gam = kk * u / (1.0 - kk * u);
-    const double e = 2.0 * gam * sqrt(nn) * (double)a.tmax_norm;
+    // fp32 accumulation (2γ_{k+2}) + the split-fp16 representation of both operands and the dropped
+    // lo·lo term (4·2^-22) + fp16 subnormal lo parts (2^-30), all relative to ‖s‖·max‖t‖
+    const double rel = 2.0 * gam + 4.0 * 2.384185791015625e-07 + 9.313225746154785e-10;
+    const double e = rel * sqrt(nn) * (double)a.tmax_norm;
     if (!((double)kth > (double)tmin + e)) {
       if (lane == 0) a.need_exact[si] = 1;
     }

@@ -67,6 +67,9 @@ struct TopkArgs {
   int kreal;
   int k;                   // requested top-k (<= 64)
   float tmax_norm;         // max_j ||T_j||_2 (for the error bound)
+  const void* Tsplit;      // [n_dst][2*KP] fp16: hi then lo halves of T[j]·2^tsc (split_rows)
+  float ssc;               // src rows are split as S[i]·2^ssc (power of two)
+  float unscale;           // 2^-(ssc + tsc): exact rescaling of the split-fp16 scores
   int32_t* cand;           // [n_src][KC] scratch
   float* cand_score;       // [n_src][KC] scratch
   int32_t* out_ids;        // [n_src][k] raw dst ids
@@ -75,6 +78,8 @@ struct TopkArgs {
 };
 hipError_t launch_topk(int KP, const TopkArgs& a, hipStream_t s);
 hipError_t launch_topk_exact(int KP, const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s);
+// out[r] = (hi, lo) fp16 split of T[r]·scale: [n][2*KP] halves (scale a power of two)
+hipError_t launch_split_rows(const float* T, int64_t n, int KP, float scale, void* out, hipStream_t s);
 // *out = bits of max_r ||T[r][0..kreal)||_2 computed in fp64
 hipError_t launch_rownorm_max(const float* T, int64_t n, int KP, int kreal, unsigned long long* out, hipStream_t s);
 constexpr int TOPK_KC = 64;  // candidates kept per src row by the MFMA pass
