@@ -1380,15 +1380,15 @@ __device__ __forceinline__ void wave_bitonic(float (&sc)[NPL], int (&ix)[NPL]) {
 // 64th) only when fewer than 64 slots remain: arrivals decay like 64/n over the scan.
 template <int KP>
 struct TopkLds {
-  static constexpr int NI = KP >= 256 ? 64 : 128, NJ = NI / 16;  // dst rows per LDS chunk
+  static constexpr int NI = 8192 / KP, NJ = NI / 16;           // dst rows per 32 KB LDS chunk
   static constexpr int RB = 4 * KP;                               // bytes per split dst row
-  static constexpr int CAP = KP >= 256 ? 160 : (KP == 128 ? 176 : 240);  // list capacity per row
-  static constexpr int NSORT = 4;                                 // sort width per lane (256 slots)
+  static constexpr int CAP = 88;                                  // list capacity per src row
+  static constexpr int NSORT = 2;                                 // sort width per lane (128 slots)
   static constexpr int CHUNK = NI * KP;                           // floats (NI * RB bytes)
   static constexpr int LISTS = 64 * CAP;                          // (score, idx) per src row
   static constexpr int FLOATS = CHUNK + 2 * LISTS + 128;          // + counts and thresholds
   static constexpr int NLD = NI * RB / 16 / 256;                  // 16-B units per thread per chunk
-  static_assert(CAP <= 64 * NSORT && CAP >= 128 && FLOATS * 4 <= 160 * 1024, "list capacity, LDS");
+  static_assert(CAP <= 64 * NSORT && CAP >= 64 + 16 && FLOATS * 4 <= 80 * 1024, "list capacity, 2 WG/CU");
 };
 __device__ __forceinline__ int tk_unit(int row, int u) { return u ^ (4 * (row & 3)); }
 
@@ -1414,7 +1414,7 @@ hipError_t launch_split_rows(const float* T, int64_t n, int KP, float scale, voi
 }
 
 template <int KP>
-__global__ __launch_bounds__(256) void topk_kernel(TopkArgs a) {
+__global__ __launch_bounds__(256, 2) void topk_kernel(TopkArgs a) {
   using TL = TopkLds<KP>;
   constexpr int NQ = KP / 32, NI = TL::NI, NJ = TL::NJ, NLD = TL::NLD, RB = TL::RB;
   constexpr int CAP = TL::CAP, NS = TL::NSORT, UPR = RB / 16;  // 16-B units per dst row
@@ -1471,7 +1471,8 @@ __global__ __launch_bounds__(256) void topk_kernel(TopkArgs a) {
       *reinterpret_cast<f32x4*>(tch + r * RB + 16 * tk_unit(r, q)) = pf[u];
     }
   };
-  float thr[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};  // rows 4g + r of this wave
+  float thr[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};  // rows 4g + r, accumulator units
+  const float rescale = 1.0f / a.unscale;  // a power of two: exact
   gload(0);
   for (int64_t j0 = 0; j0 < a.n_dst; j0 += NI) {
     __syncthreads();  // previous chunk consumed
@@ -1494,51 +1495,54 @@ __global__ __launch_bounds__(256) void topk_kernel(TopkArgs a) {
         acc[J] = mfma_h(ul[q], th, acc[J]);
       }
     }
-    // append candidates 64 dst rows at a time (a list holds <= CAP-64 kept + 64 new): lane holds
-    // src rows 4g + r (of this wave's 16), dst j0 + 16J + i16; thresholds live in registers
-    static_for<0, NJ / 4>([&](auto hh) {
-      constexpr int h = decltype(hh)::value;
+    // append candidates 16 dst rows at a time (a list holds <= CAP-16 kept + 16 new): lane holds
+    // src rows 4g + r (of this wave's 16), dst j0 + 16J + i16.  Thresholds live in registers in
+    // the scaled units of the accumulators (thr · 2^(ssc+tsc), exact); appends and the compaction
+    // check only run when some lane beats its threshold (rare once the lists have filled).
+    static_for<0, NJ>([&](auto JJ) {
+      constexpr int J = decltype(JJ)::value;
+      bool hit = false;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int sr = 4 * g + r;
+      for (int r = 0; r < 4; ++r) hit |= acc[J][r] >= thr[r];
+      if (__any(hit)) {
+        const int64_t dj = j0 + 16 * J + i16;
 #pragma unroll
-        for (int J = 4 * h; J < 4 * h + 4; ++J) {
-          const int64_t dj = j0 + 16 * J + i16;
-          const float sc = acc[J][r] * a.unscale;
-          if (dj < a.n_dst && sc >= thr[r]) {
+        for (int r = 0; r < 4; ++r) {
+          const int sr = 4 * g + r;
+          if (dj < a.n_dst && acc[J][r] >= thr[r]) {
             const int pos = atomicAdd(&wcnt[sr], 1);
-            wsc[sr * CAP + pos] = sc;
+            wsc[sr * CAP + pos] = acc[J][r] * a.unscale;
             wix[sr * CAP + pos] = (int)dj;
           }
         }
-      }
-      WAVE_LDS_SYNC();
-      // compact the rows that could overflow on the next 64 (best 64 kept, threshold = the 64th)
-      const int mycnt = lane < 16 ? wcnt[lane] : 0;
-      unsigned long long full = __ballot(mycnt > CAP - 64);
-      if (full) {
-        while (full) {
-          const int sr = __builtin_ctzll(full);
-          full &= full - 1;
-          const int cnt = rdlane_i(mycnt, sr);
-          float s2[NS];
-          int i2[NS];
+        WAVE_LDS_SYNC();
+        // compact the rows that could overflow on the next 16 (best 64 kept, threshold = the 64th)
+        const int mycnt = lane < 16 ? wcnt[lane] : 0;
+        unsigned long long full = __ballot(mycnt > CAP - 16);
+        if (full) {
+          while (full) {
+            const int sr = __builtin_ctzll(full);
+            full &= full - 1;
+            const int cnt = rdlane_i(mycnt, sr);
+            float s2[NS];
+            int i2[NS];
 #pragma unroll
-          for (int q = 0; q < NS; ++q) {
-            const int e = lane + 64 * q;
-            s2[q] = e < cnt ? wsc[sr * CAP + e] : -INFINITY;
-            i2[q] = e < cnt ? wix[sr * CAP + e] : -1;
+            for (int q = 0; q < NS; ++q) {
+              const int e = lane + 64 * q;
+              s2[q] = e < cnt ? wsc[sr * CAP + e] : -INFINITY;
+              i2[q] = e < cnt ? wix[sr * CAP + e] : -1;
+            }
+            wave_bitonic<NS>(s2, i2);
+            WAVE_LDS_SYNC();
+            wsc[sr * CAP + lane] = s2[0];
+            wix[sr * CAP + lane] = i2[0];
+            if (lane == 63) wthr[sr] = s2[0];
+            if (lane == 0) wcnt[sr] = 64;
+            WAVE_LDS_SYNC();
           }
-          wave_bitonic<NS>(s2, i2);
-          WAVE_LDS_SYNC();
-          wsc[sr * CAP + lane] = s2[0];
-          wix[sr * CAP + lane] = i2[0];
-          if (lane == 63) wthr[sr] = s2[0];
-          if (lane == 0) wcnt[sr] = 64;
-          WAVE_LDS_SYNC();
-        }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) thr[r] = wthr[4 * g + r];
+          for (int r = 0; r < 4; ++r) thr[r] = wthr[4 * g + r] * rescale;
+        }
       }
     });
   }
