@@ -111,33 +111,40 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int64_t r
     acc[s] = zero4();
     for (int r = 0; r < 4; ++r) acc64[s][r] = 0.0;
   }
-  int cnt = 0;
-  for (int64_t r0 = rb; r0 < re; r0 += 4) {
-    const int64_t row = r0 + g;
-    f32x4 v[NH];
+  // 16 rows per trip: the four 4-row groups' loads are all in flight before the first MFMA
+  for (int64_t r0 = rb; r0 < re; r0 += 64) {
+    const int64_t r1 = r0 + 64 < re ? r0 + 64 : re;
+    for (int64_t q0 = r0; q0 < r1; q0 += 16) {
+      f32x4 v[4][NH];
 #pragma unroll
-    for (int h = 0; h < NH; ++h) v[h] = row < re ? ld4(X + row * KP + 64 * h + 4 * i16) : zero4();
-    static_for<0, NTW>([&](auto s) {
-      constexpr int t = W + NWV * decltype(s)::value;
-      if constexpr (t < NT) {
-        constexpr TilePair p = upper_tile(t, NQ);
-        acc[s] = mfma4(v[p.a >> 2][p.a & 3], v[p.b >> 2][p.b & 3], acc[s]);
-      }
-    });
-    if (++cnt == 16) {  // 64 rows per fp32 partial, then fp64 (Spark accumulates in fp64)
-      cnt = 0;
+      for (int d = 0; d < 4; ++d)
 #pragma unroll
-      for (int s = 0; s < NTW; ++s) {
-        for (int r = 0; r < 4; ++r) acc64[s][r] += (double)acc[s][r];
-        acc[s] = zero4();
-      }
+        for (int h = 0; h < NH; ++h) {
+          const int64_t row = q0 + 4 * d + g;
+          v[d][h] = row < r1 ? ld4(X + row * KP + 64 * h + 4 * i16) : zero4();
+        }
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+        static_for<0, NTW>([&](auto s) {
+          constexpr int t = W + NWV * decltype(s)::value;
+          if constexpr (t < NT) {
+            constexpr TilePair p = upper_tile(t, NQ);
+            acc[s] = mfma4(v[d][p.a >> 2][p.a & 3], v[d][p.b >> 2][p.b & 3], acc[s]);
+          }
+        });
+    }
+    // 64 rows per fp32 partial, then fp64 (Spark accumulates in fp64)
+#pragma unroll
+    for (int s = 0; s < NTW; ++s) {
+      for (int r = 0; r < 4; ++r) acc64[s][r] += (double)acc[s][r];
+      acc[s] = zero4();
     }
   }
 #pragma unroll
   for (int s = 0; s < NTW; ++s) {
     const int t = W + NWV * s;
     if (t < NT)
-      for (int r = 0; r < 4; ++r) out[((size_t)t * 64 + lane) * 4 + r] = acc64[s][r] + (double)acc[s][r];
+      for (int r = 0; r < 4; ++r) out[((size_t)t * 64 + lane) * 4 + r] = acc64[s][r];
   }
 }
 
