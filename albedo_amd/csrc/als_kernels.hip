@@ -319,19 +319,21 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
   f32x4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = zero4();
+  // D^-1/2 of the row, one rsq per column (lane c, c+64, ...) into this wave's LDS slot
+  float* sdl = smem + 4 * D * LDK + wave * KP;
   bool bad = false;
+#pragma unroll
+  for (int h = 0; h < NHC; ++h) {
+    const int cc = lane + 64 * h;
+    const float dd = a.lam[cc] + lamn;
+    if (cc < a.kreal && !(dd > 0.f)) bad = true;
+    sdl[cc] = (cc < a.kreal && dd > 0.f) ? frsq(dd) : 0.f;
+  }
+  WAVE_LDS_SYNC();
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int c0 = 16 * c;
-    const f32x4 dl = ld4(a.lam + c0 + 4 * g);
-    float sd[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int cc = c0 + 4 * g + m;
-      const float dd = dl[m] + lamn;
-      if (cc < a.kreal && !(dd > 0.f)) bad = true;
-      sd[m] = (cc < a.kreal && dd > 0.f) ? frsq(dd) : 0.f;
-    }
+    const f32x4 sd = ld4(sdl + c0 + 4 * g);
     f32x4 z[NB];
 #pragma unroll
     for (int I = 0; I < NB; ++I) {
@@ -375,8 +377,10 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
   float dg = 1.f;  // 1 / L[me][me]
   float y = valid ? we * cinv : 0.f;
   if constexpr (D == 16) {
+    // rows c >= d are identity rows (and y_c = 0): their steps change nothing and are skipped
     static_for<0, D>([&](auto cc) {
       constexpr int c = decltype(cc)::value;
+      if (c >= d) return;
       const float piv = bc16<c>(kr[c]);
       if (!(piv > 0.f)) notpd = true;
       const float inv = frsq(piv), s = piv * inv;
@@ -389,6 +393,7 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
     });
     static_for<0, D>([&](auto cc) {
       constexpr int c = decltype(cc)::value;
+      if (c >= d) return;
       const float yc = bc16<c>(y * dg);
       y = (me > c) ? fmaf(-kr[c], yc, y) : ((me == c) ? yc : y);
     });
@@ -424,6 +429,7 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
   if constexpr (D == 16) {
     static_for<0, D>([&](auto cc) {
       constexpr int c = D - 1 - decltype(cc)::value;
+      if (c >= d) return;
       const float vc = bc16<c>(y * dg);
       y = (me < c) ? fmaf(-lt[c], vc, y) : ((me == c) ? vc : y);
     });
@@ -450,16 +456,9 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
       for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) pr[m] += __shfl_xor(pr[m], o);
-      if (i16 == 0) {
-        const f32x4 dl = ld4(a.lam + 16 * c + 4 * g);
-        f32x4 o4;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const int cc = 16 * c + 4 * g + m;
-          const float dd = dl[m] + lamn;
-          o4[m] = (cc < a.kreal && dd > 0.f) ? pr[m] * frcp(dd) : 0.f;
-        }
-        *reinterpret_cast<f32x4*>(a.X + (int64_t)j * KP + 16 * c + 4 * g) = o4;
+      if (i16 == 0) {  // D^-1 = (D^-1/2)^2 (zero on padded / invalid columns)
+        const f32x4 sd = ld4(sdl + 16 * c + 4 * g);
+        *reinterpret_cast<f32x4*>(a.X + (int64_t)j * KP + 16 * c + 4 * g) = pr * (sd * sd);
       }
     }
   } else {
@@ -485,8 +484,8 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
 #pragma unroll
     for (int h = 0; h < NHC; ++h) {
       const int c = lane + 64 * h;
-      const float dd = a.lam[c] + lamn;
-      a.X[(int64_t)j * KP + c] = (c < a.kreal && dd > 0.f) ? xacc[h] * frcp(dd) : 0.f;
+      const float sd = sdl[c];
+      a.X[(int64_t)j * KP + c] = xacc[h] * (sd * sd);
     }
   }
 }
@@ -494,7 +493,7 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
 hipError_t launch_solve_light(int KP, int D, const SolveArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;
   const int blocks = (int)((a.n_rows + 3) / 4);
-  const size_t lds = (size_t)4 * D * (D + 1) * sizeof(float);
+  const size_t lds = ((size_t)4 * D * (D + 1) + (size_t)4 * KP) * sizeof(float);  // K per wave + D^-1/2
 #define LIGHT(kp, dd) \
   if (KP == kp && D == dd) { solve_light_kernel<kp, dd><<<blocks, 256, lds, s>>>(a); return hipGetLastError(); }
   LIGHT(64, 16) LIGHT(64, 32) LIGHT(64, 64) LIGHT(128, 16) LIGHT(128, 32) LIGHT(128, 64)

@@ -15,17 +15,19 @@ namespace albedo {
 // as in the public-domain JAMA formulation).  a: n x n row-major symmetric.  On return w holds the
 // eigenvalues ascending and v (row-major) the eigenvectors as columns: a = v diag(w) vᵀ.
 // ---------------------------------------------------------------------------------------------
+// (transposed storage: V[c * n + r] holds element (r, c), so the column sweeps of the JAMA code
+// run along contiguous rows; the input is symmetric, the output is the transformation transposed)
 static void tred2(int n, double* V, double* d, double* e) {
-  for (int j = 0; j < n; j++) d[j] = V[(n - 1) * n + j];
+  for (int j = 0; j < n; j++) d[j] = V[j * n + (n - 1)];
   for (int i = n - 1; i > 0; i--) {
     double scale = 0.0, h = 0.0;
     for (int k = 0; k < i; k++) scale += std::fabs(d[k]);
     if (scale == 0.0) {
       e[i] = d[i - 1];
       for (int j = 0; j < i; j++) {
-        d[j] = V[(i - 1) * n + j];
-        V[i * n + j] = 0.0;
+        d[j] = V[j * n + (i - 1)];
         V[j * n + i] = 0.0;
+        V[i * n + j] = 0.0;
       }
     } else {
       for (int k = 0; k < i; k++) {
@@ -41,11 +43,11 @@ static void tred2(int n, double* V, double* d, double* e) {
       for (int j = 0; j < i; j++) e[j] = 0.0;
       for (int j = 0; j < i; j++) {
         f = d[j];
-        V[j * n + i] = f;
+        V[i * n + j] = f;
         g = e[j] + V[j * n + j] * f;
         for (int k = j + 1; k <= i - 1; k++) {
-          g += V[k * n + j] * d[k];
-          e[k] += V[k * n + j] * f;
+          g += V[j * n + k] * d[k];
+          e[k] += V[j * n + k] * f;
         }
         e[j] = g;
       }
@@ -59,32 +61,32 @@ static void tred2(int n, double* V, double* d, double* e) {
       for (int j = 0; j < i; j++) {
         f = d[j];
         g = e[j];
-        for (int k = j; k <= i - 1; k++) V[k * n + j] -= (f * e[k] + g * d[k]);
-        d[j] = V[(i - 1) * n + j];
-        V[i * n + j] = 0.0;
+        for (int k = j; k <= i - 1; k++) V[j * n + k] -= (f * e[k] + g * d[k]);
+        d[j] = V[j * n + (i - 1)];
+        V[j * n + i] = 0.0;
       }
     }
     d[i] = h;
   }
   for (int i = 0; i < n - 1; i++) {
-    V[(n - 1) * n + i] = V[i * n + i];
+    V[i * n + (n - 1)] = V[i * n + i];
     V[i * n + i] = 1.0;
     const double h = d[i + 1];
     if (h != 0.0) {
-      for (int k = 0; k <= i; k++) d[k] = V[k * n + i + 1] / h;
+      for (int k = 0; k <= i; k++) d[k] = V[(i + 1) * n + k] / h;
       for (int j = 0; j <= i; j++) {
         double g = 0.0;
-        for (int k = 0; k <= i; k++) g += V[k * n + i + 1] * V[k * n + j];
-        for (int k = 0; k <= i; k++) V[k * n + j] -= g * d[k];
+        for (int k = 0; k <= i; k++) g += V[(i + 1) * n + k] * V[j * n + k];
+        for (int k = 0; k <= i; k++) V[j * n + k] -= g * d[k];
       }
     }
-    for (int k = 0; k <= i; k++) V[k * n + i + 1] = 0.0;
+    for (int k = 0; k <= i; k++) V[(i + 1) * n + k] = 0.0;
   }
   for (int j = 0; j < n; j++) {
-    d[j] = V[(n - 1) * n + j];
-    V[(n - 1) * n + j] = 0.0;
+    d[j] = V[j * n + (n - 1)];
+    V[j * n + (n - 1)] = 0.0;
   }
-  V[(n - 1) * n + n - 1] = 1.0;
+  V[(n - 1) * n + (n - 1)] = 1.0;
   e[0] = 0.0;
 }
 
@@ -130,10 +132,12 @@ static bool tql2(int n, double* V, double* d, double* e) {
           c = p / r;
           p = c * d[i] - s * g;
           d[i + 1] = h + s * (c * g + s * d[i]);
+          double* __restrict__ vi = V + (size_t)i * n;  // V holds the vectors as rows here
+          double* __restrict__ vi1 = vi + n;
           for (int k = 0; k < n; k++) {
-            h = V[k * n + i + 1];
-            V[k * n + i + 1] = s * V[k * n + i] + c * h;
-            V[k * n + i] = c * V[k * n + i] - s * h;
+            h = vi1[k];
+            vi1[k] = s * vi[k] + c * h;
+            vi[k] = c * vi[k] - s * h;
           }
         }
         p = -s * s2 * c3 * el1 * e[l] / dl1;
@@ -155,10 +159,15 @@ static bool tql2(int n, double* V, double* d, double* e) {
     if (k != i) {
       d[k] = d[i];
       d[i] = p;
-      for (int j = 0; j < n; j++) std::swap(V[j * n + i], V[j * n + k]);
+      for (int j = 0; j < n; j++) std::swap(V[(size_t)i * n + j], V[(size_t)k * n + j]);
     }
   }
   return true;
+}
+
+static void transpose(int n, double* V) {
+  for (int i = 0; i < n; i++)
+    for (int j = i + 1; j < n; j++) std::swap(V[(size_t)i * n + j], V[(size_t)j * n + i]);
 }
 
 bool sym_eig(int n, const double* a, double* w, double* v) {
@@ -169,8 +178,10 @@ bool sym_eig(int n, const double* a, double* w, double* v) {
     v[0] = 1.0;
     return true;
   }
-  tred2(n, v, w, e.data());
-  return tql2(n, v, w, e.data());
+  tred2(n, v, w, e.data());  // leaves the transformation transposed: vectors as rows
+  const bool ok = tql2(n, v, w, e.data());  // QL rotations on contiguous rows
+  transpose(n, v);
+  return ok;
 }
 
 // ---------------------------------------------------------------------------------------------
