@@ -211,36 +211,51 @@ hipError_t launch_gram(int KP, const float* X, int64_t n, double* slab, int nblk
 // =============================================================================================
 template <int KP> constexpr int rotate_cols() { return KP >= 256 ? 128 : KP; }  // output columns per block
 
+// 8 waves per block share one LDS copy of M (64+ KB); each wave's
+// 16 rows are loaded whole before the first MFMA.
+constexpr int ROT_WAVES = 8;
 template <int KP>
-__global__ __launch_bounds__(256) void rotate_kernel(const float* __restrict__ X, const float* __restrict__ M,
-                                                     float* __restrict__ Z, int64_t n) {
-  constexpr int NO = rotate_cols<KP>(), LDM = NO + 4, NJ = NO / 16;
+__global__ __launch_bounds__(64 * ROT_WAVES) void rotate_kernel(const float* __restrict__ X,
+                                                               const float* __restrict__ M,
+                                                               float* __restrict__ Z, int64_t n) {
+  constexpr int NO = rotate_cols<KP>(), LDM = NO + 4, NJ = NO / 16, NC = KP / 16;
+  constexpr int NTH = 64 * ROT_WAVES, RPB = 16 * ROT_WAVES;  // rows per block iteration
   extern __shared__ __attribute__((aligned(16))) float sM[];
   const int co = blockIdx.y * NO;  // this block's output columns co .. co+NO-1
-  for (int e = threadIdx.x; e < KP * NO / 4; e += 256) {
+  for (int e = threadIdx.x; e < KP * NO / 4; e += NTH) {
     const int r = (4 * e) / NO, c = (4 * e) % NO;
     *reinterpret_cast<f32x4*>(sM + r * LDM + c) = ld4(M + r * KP + co + c);
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
-  for (int64_t b = blockIdx.x; b * 64 < n; b += gridDim.x) {
-    const int64_t row = b * 64 + wave * 16 + i16;
+  for (int64_t b = blockIdx.x; b * RPB < n; b += gridDim.x) {
+    const int64_t row = b * RPB + wave * 16 + i16;
+    constexpr bool PRE = KP <= 128;  // whole-row preload (KP = 256: per slice, registers)
+    f32x4 a4[PRE ? NC : 1];
+    if constexpr (PRE) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) a4[c] = row < n ? ld4(X + row * KP + 16 * c + 4 * g) : zero4();
+    }
     f32x4 acc[NJ];
 #pragma unroll
     for (int J = 0; J < NJ; ++J) acc[J] = zero4();
-    for (int c0 = 0; c0 < KP; c0 += 16) {
-      const f32x4 a4 = row < n ? ld4(X + row * KP + c0 + 4 * g) : zero4();
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      f32x4 av;
+      if constexpr (PRE) av = a4[c];
+      else av = row < n ? ld4(X + row * KP + 16 * c + 4 * g) : zero4();
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-        const float* mr = sM + (c0 + 4 * g + m) * LDM + i16;
+        const float* mr = sM + (16 * c + 4 * g + m) * LDM + i16;
 #pragma unroll
-        for (int J = 0; J < NJ; ++J) acc[J] = mfma4(a4[m], mr[16 * J], acc[J]);
+        for (int J = 0; J < NJ; ++J) acc[J] = mfma4(av[m], mr[16 * J], acc[J]);
       }
+      __builtin_amdgcn_sched_barrier(0);  // one 16-column slice of M in registers at a time
     }
 #pragma unroll
     for (int J = 0; J < NJ; ++J)
       for (int r = 0; r < 4; ++r) {
-        const int64_t rr = b * 64 + wave * 16 + 4 * g + r;
+        const int64_t rr = b * RPB + wave * 16 + 4 * g + r;
         if (rr < n) Z[rr * KP + co + 16 * J + i16] = acc[J][r];
       }
   }
@@ -248,15 +263,22 @@ __global__ __launch_bounds__(256) void rotate_kernel(const float* __restrict__ X
 
 hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  int64_t blocks = (n + 63) / 64;
-  if (blocks > 2048) blocks = 2048;
-  if (KP == 64) rotate_kernel<64><<<(int)blocks, 256, (size_t)64 * 68 * 4, s>>>(X, M, Z, n);
-  else if (KP == 128) rotate_kernel<128><<<(int)blocks, 256, (size_t)128 * 132 * 4, s>>>(X, M, Z, n);
-  else if (KP == 256) {
+  int64_t blocks = (n + 16 * ROT_WAVES - 1) / (16 * ROT_WAVES);
+  if (blocks > 1024) blocks = 1024;
+  const int nth = 64 * ROT_WAVES;
+  if (KP == 64) {
+    const size_t lds = (size_t)64 * 68 * 4;
+    rotate_kernel<64><<<(int)blocks, nth, lds, s>>>(X, M, Z, n);
+  } else if (KP == 128) {
+    const size_t lds = (size_t)128 * 132 * 4;
+    static const hipError_t attr = allow_lds(rotate_kernel<128>, lds);
+    if (attr != hipSuccess) return attr;
+    rotate_kernel<128><<<(int)blocks, nth, lds, s>>>(X, M, Z, n);
+  } else if (KP == 256) {
     const size_t lds = (size_t)256 * (rotate_cols<256>() + 4) * 4;
     static const hipError_t attr = allow_lds(rotate_kernel<256>, lds);
     if (attr != hipSuccess) return attr;
-    rotate_kernel<256><<<dim3((int)blocks, 256 / rotate_cols<256>()), 256, lds, s>>>(X, M, Z, n);
+    rotate_kernel<256><<<dim3((int)blocks, 256 / rotate_cols<256>()), nth, lds, s>>>(X, M, Z, n);
   } else return hipErrorInvalidValue;
   return hipGetLastError();
 }
