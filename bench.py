@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIG_RANK))
-    ap.add_argument("--topk-users", type=int, default=16384)
+    ap.add_argument("--topk-users", type=int, default=65536)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--light", type=int, default=-1)
