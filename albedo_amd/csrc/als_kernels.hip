@@ -57,6 +57,13 @@ __device__ __forceinline__ float bc16(float v) {
 __device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x4 mfma_h(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
 template <int I, int N, typename F>
@@ -352,28 +359,71 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
     sdl[cc] = (cc < a.kreal && dd > 0.f) ? frsq(dd) : 0.f;
   }
   WAVE_LDS_SYNC();
+  if constexpr (D == 64) {
+    // S on split-fp16 MFMA (hi·hi + hi·lo + lo·hi, 32 columns per instruction: 120 instead of 320
+    // fp32 MFMAs).  One power-of-two scale for the whole row (so S unscales exactly):
+    // |Z[.][c]| < 2^(13 - e_c) (colscale), hence |z_c · sd_c| <= max_c sd_c · 2^(13 - e_c).
+    float bnd = 0.f;
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const int c0 = 16 * c;
-    const f32x4 sd = ld4(sdl + c0 + 4 * g);
-    f32x4 z[NB];
-#pragma unroll
-    for (int I = 0; I < NB; ++I) {
-      if constexpr (KEEPZ) z[I] = zf[I][c];
-      else z[I] = vB[I] ? ld4(a.Z + (int64_t)colB[I] * KP + c0 + 4 * g) : zero4();
-#pragma unroll
-      for (int m = 0; m < 4; ++m) z[I][m] *= sd[m];
+    for (int h = 0; h < NHC; ++h) {
+      const int cc = lane + 64 * h;
+      bnd = fmaxf(bnd, sdl[cc] * a.colscale[KP + cc]);
     }
+    for (int o = 32; o > 0; o >>= 1) bnd = fmaxf(bnd, __shfl_xor(bnd, o));
+    int ex = 0;
+    frexpf(bnd * 8192.f, &ex);  // bnd·2^13 < 2^ex
+    const float sc = ldexpf(1.f, 13 - ex), usc = ldexpf(1.f, 2 * (ex - 13));
+    constexpr int NQ = KP / 32;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+    for (int q = 0; q < NQ; ++q) {
+      const f32x4 s0 = ld4(sdl + 32 * q + 8 * g), s1 = ld4(sdl + 32 * q + 8 * g + 4);
+      f16x8 zh[NB], zl[NB];
+#pragma unroll
+      for (int I = 0; I < NB; ++I) {
+        const float* zp = a.Z + (int64_t)colB[I] * KP + 32 * q + 8 * g;
+        const f32x4 v0 = vB[I] ? ld4(zp) : zero4(), v1 = vB[I] ? ld4(zp + 4) : zero4();
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float v = (e < 4 ? v0[e] * s0[e] : v1[e - 4] * s1[e - 4]) * sc;
+          asm("" : "+v"(v));  // one fp32 rounding; hi and lo from that value (see lds_put)
+          const _Float16 hv = (_Float16)v;
+          zh[I][e] = hv;
+          zl[I][e] = (_Float16)(v - (float)hv);
+        }
+      }
       static_for<0, NT>([&](auto t) {
         constexpr TilePair p = upper_tile(decltype(t)::value, NB);
-        acc[t] = mfma4(z[p.a][m], z[p.b][m], acc[t]);
+        acc[t] = mfma_h(zh[p.a], zh[p.b], acc[t]);
+        acc[t] = mfma_h(zh[p.a], zl[p.b], acc[t]);
+        acc[t] = mfma_h(zl[p.a], zh[p.b], acc[t]);
       });
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] *= usc;
+  } else {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int c0 = 16 * c;
+      const f32x4 sd = ld4(sdl + c0 + 4 * g);
+      f32x4 z[NB];
+#pragma unroll
+      for (int I = 0; I < NB; ++I) {
+        if constexpr (KEEPZ) z[I] = zf[I][c];
+        else z[I] = vB[I] ? ld4(a.Z + (int64_t)colB[I] * KP + c0 + 4 * g) : zero4();
+#pragma unroll
+        for (int m = 0; m < 4; ++m) z[I][m] *= sd[m];
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        static_for<0, NT>([&](auto t) {
+          constexpr TilePair p = upper_tile(decltype(t)::value, NB);
+          acc[t] = mfma4(z[p.a][m], z[p.b][m], acc[t]);
+        });
+      }
     }
   }
   if (__any(bad) && lane == 0) atomicOr(a.err, 1);
-  // S -> LDS (symmetric operands make S bitwise symmetric, so mirrored writes agree)
+  // S -> LDS (only the lower triangle is read by the Cholesky below)
   static_for<0, NT>([&](auto t) {
     constexpr TilePair p = upper_tile(decltype(t)::value, NB);
 #pragma unroll
@@ -549,13 +599,6 @@ constexpr int HT_LD = 17, HT_SZ = 16 * HT_LD;
 __device__ __forceinline__ int htile(int I, int J) { return (I * (I + 1) / 2 + J) * HT_SZ; }
 __device__ __forceinline__ int hel(int r, int c) { return htile(r >> 4, c >> 4) + (r & 15) * HT_LD + (c & 15); }
 
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ f32x4 mfma_h(f16x8 a, f16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-}
 
 template <int KP>
 struct Heavy {
