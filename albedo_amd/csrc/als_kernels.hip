@@ -52,6 +52,16 @@ __device__ __forceinline__ float bc16(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + M, 0xF, 0xF, true));
 }
 
+// Sum over each 16-lane row, result in the row's lane 15: DPP row_shr prefix sums (VALU only; a
+// __shfl_xor butterfly goes through the LDS crossbar instead).
+__device__ __forceinline__ float sum16_last(float x) {
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x111, 0xF, 0xF, true));  // row_shr:1
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x112, 0xF, 0xF, true));  // row_shr:2
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x114, 0xF, 0xF, true));  // row_shr:4
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x118, 0xF, 0xF, true));  // row_shr:8
+  return x;
+}
+
 // v_rsq_f32 / v_rcp_f32 / v_sqrt_f32: single instructions (~1 ulp) instead of the IEEE-exact
 // multi-instruction expansions; the solve tolerance is 1e-4 relative (tests state it)
 __device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
@@ -525,10 +535,8 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
 #pragma unroll
       for (int I = 1; I < NB; ++I) pr += zf[I][c] * vI[I];
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) pr[m] += __shfl_xor(pr[m], o);
-      if (i16 == 0) {  // D^-1 = (D^-1/2)^2 (zero on padded / invalid columns)
+      for (int m = 0; m < 4; ++m) pr[m] = sum16_last(pr[m]);
+      if (i16 == 15) {  // D^-1 = (D^-1/2)^2 (zero on padded / invalid columns)
         const f32x4 sd = ld4(sdl + 16 * c + 4 * g);
         *reinterpret_cast<f32x4*>(a.X + (int64_t)j * KP + 16 * c + 4 * g) = pr * (sd * sd);
       }
