@@ -52,6 +52,29 @@ __device__ __forceinline__ float bc16(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + M, 0xF, 0xF, true));
 }
 
+// acc -= (v of lane M of the 16-lane row) * w in ONE instruction (v_fmac_f32 with a DPP
+// row_newbcast source; the compiler keeps the broadcast as a separate v_mov_b32_dpp).  Same single
+// rounding as fmaf(-w, bc16<M>(v), acc).  NOP: v may have been written by the previous VALU
+// instruction (a DPP source needs 2 wait states, which the compiler does not insert around asm);
+// volatile keeps these in program order, so only the first use after a write needs it.
+template <int M, bool NOP>
+__device__ __forceinline__ void fnmac_bc16(float& acc, float v, float w) {
+  if constexpr (NOP)
+    asm volatile("s_nop 1\n\tv_fmac_f32_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+                 : "+v"(acc) : "v"(v), "v"(w), "n"(M));
+  else
+    asm volatile("v_fmac_f32_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+                 : "+v"(acc) : "v"(v), "v"(w), "n"(M));
+}
+// bc16 for a source written by asm (fnmac_bc16): the wait states are explicit
+template <int M>
+__device__ __forceinline__ float bc16_after_asm(float v) {
+  float r;
+  asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+               : "=v"(r) : "v"(v), "n"(M));
+  return r;
+}
+
 // Sum over each 16-lane row, result in the row's lane 15: DPP row_shr prefix sums (VALU only; a
 // __shfl_xor butterfly goes through the LDS crossbar instead).
 __device__ __forceinline__ float sum16_last(float x) {
@@ -463,14 +486,14 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
     static_for<0, D>([&](auto cc) {
       constexpr int c = decltype(cc)::value;
       if (c >= d) return;
-      const float piv = bc16<c>(kr[c]);
+      const float piv = bc16_after_asm<c>(kr[c]);
       if (!(piv > 0.f)) notpd = true;
       const float inv = frsq(piv), s = piv * inv;
       kr[c] = (me == c) ? s : kr[c] * inv;
       dg = (me == c) ? inv : dg;
       static_for<c + 1, D>([&](auto mm) {
         constexpr int m = decltype(mm)::value;
-        kr[m] = fmaf(-kr[c], bc16<m>(kr[c]), kr[m]);
+        fnmac_bc16<m, m == c + 1>(kr[m], kr[c], kr[c]);
       });
     });
     static_for<0, D>([&](auto cc) {
@@ -847,13 +870,13 @@ __device__ __forceinline__ bool chol16(float (&rr)[16], float& dg, int i) {
   static_for<0, 16>([&](auto cc) {
     constexpr int c = decltype(cc)::value;
     if (i == c && !(rr[c] > d0 * 4.76837158e-07f)) notpd = true;
-    const float piv = bc16<c>(rr[c]);
+    const float piv = bc16_after_asm<c>(rr[c]);
     const float inv = frsq(piv), sq = piv * inv;
     rr[c] = (i == c) ? sq : rr[c] * inv;
     dg = (i == c) ? inv : dg;
     static_for<c + 1, 16>([&](auto mm) {
       constexpr int m = decltype(mm)::value;
-      rr[m] = fmaf(-rr[c], bc16<m>(rr[c]), rr[m]);
+      fnmac_bc16<m, m == c + 1>(rr[m], rr[c], rr[c]);
     });
   });
   return __any(notpd);
