@@ -82,13 +82,56 @@ def mean_average_precision(pairs):
 
 
 class RankingEvaluator:
+    """RankingEvaluator.scala:14-108.  The per-user item lists are dicts {user: [items]} (the output
+    of `into_user_items`), standing in for the (userCol, itemsCol) DataFrames."""
+
+    _METRICS = ("NDCG@k", "Precision@k", "MAP")
+
     def __init__(self, user_actual_items: dict, metric_name="NDCG@k", k=15):
         self.actual = user_actual_items
         self.metric_name = metric_name
         self.k = k
+        self.user_col = "user"
+        self.items_col = "items"
 
-    def formatted_metric_name(self):
+    # Spark-style params (:21-49)
+    def setMetricName(self, v):
+        if v not in self._METRICS:
+            raise ValueError(f"unsupported metric {v}; supports {', '.join(self._METRICS)}")
+        self.metric_name = v
+        return self
+
+    def getMetricName(self):
+        return self.metric_name
+
+    def setK(self, v):
+        self.k = int(v)
+        return self
+
+    def getK(self):
+        return self.k
+
+    def setUserCol(self, v):
+        self.user_col = v
+        return self
+
+    def getUserCol(self):
+        return self.user_col
+
+    def setItemsCol(self, v):
+        self.items_col = v
+        return self
+
+    def getItemsCol(self):
+        return self.items_col
+
+    def isLargerBetter(self):
+        return True
+
+    def getFormattedMetricName(self):
         return self.metric_name.replace("@k", f"@{self.k}")
+
+    formatted_metric_name = getFormattedMetricName
 
     def evaluate(self, user_predicted_items: dict) -> float:
         pairs = [(user_predicted_items[u][: self.k], self.actual[u][: self.k])
