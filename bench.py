@@ -29,7 +29,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-CONFIG_RANK = {"c2": 64, "c4": 128, "c1p": 50}
+CONFIG_RANK = {"c2": 64, "c4": 128, "c1p": 50, "c5": 256}
+NONNEGATIVE = {"c5"}  # BASELINE config 5: rank 256, nonnegative=true (NNLS), extreme repo skew
 METRIC = "implicit-ALS interactions/sec per sweep at rank 128 (1/8 GPU); top-30 recs users/sec"
 
 
@@ -65,6 +66,7 @@ def main():
     p = L.als_params()
     L.check(lib.als_params_default(C.byref(p)))
     p.rank, p.implicit_prefs, p.reg_param, p.alpha, p.seed = k, 1, 0.5, 40.0, 42
+    p.nonnegative = 1 if args.config in NONNEGATIVE else 0
     p.device = local
     p.light_max_degree = args.light
     h = C.c_void_p()
