@@ -120,43 +120,64 @@ def _make_accessors(cls):
 class ALS(_Params):
     """Spark ml.recommendation.ALS (estimator)."""
 
-    def _c_params(self):
+    def _c_params(self, pm=None):
+        v = dict(self._p)
+        if pm:
+            v.update(pm)
         p = _lib.als_params()
         check(load().als_params_default(C.byref(p)))
-        p.rank = int(self._p["rank"])
-        p.max_iter = int(self._p["maxIter"])
-        p.implicit_prefs = 1 if self._p["implicitPrefs"] else 0
-        p.nonnegative = 1 if self._p["nonnegative"] else 0
-        p.num_user_blocks = int(self._p["numUserBlocks"])
-        p.num_item_blocks = int(self._p["numItemBlocks"])
-        p.reg_param = float(self._p["regParam"])
-        p.alpha = float(self._p["alpha"])
-        p.seed = int(self._p["seed"])
-        p.device = int(self._p["device"])
-        p.light_max_degree = int(self._p["lightMaxDegree"])
+        p.rank = int(v["rank"])
+        p.max_iter = int(v["maxIter"])
+        p.implicit_prefs = 1 if v["implicitPrefs"] else 0
+        p.nonnegative = 1 if v["nonnegative"] else 0
+        p.num_user_blocks = int(v["numUserBlocks"])
+        p.num_item_blocks = int(v["numItemBlocks"])
+        p.reg_param = float(v["regParam"])
+        p.alpha = float(v["alpha"])
+        p.seed = int(v["seed"])
+        p.device = int(v["device"])
+        p.light_max_degree = int(v["lightMaxDegree"])
         return p
 
-    def _context(self):
+    def _context(self, pm=None):
         lib = load()
-        p = self._c_params()
+        p = self._c_params(pm)
         h = C.c_void_p()
         check(lib.als_create(C.byref(p), C.byref(h)))
         return h
 
-    def fit(self, dataset, initialUserFactors=None, initialItemFactors=None) -> "ALSModel":
-        """ALS.fit. `initial*Factors` = (ids, factors[n, rank]) injects the start point (parity path);
-        without it the Spark-style XORShiftRandom initialisation is used."""
-        user = _checked_cast(_column(dataset, self._p["userCol"]), self._p["userCol"])
-        item = _checked_cast(_column(dataset, self._p["itemCol"]), self._p["itemCol"])
-        rating = np.ascontiguousarray(_column(dataset, self._p["ratingCol"]), dtype=np.float32)
+    def _param_map(self, pm):
+        """Validate a ParamMap (dict of param name -> value) like Params.copy(extra)."""
+        probe = ALS(**self._p)
+        for k, v in pm.items():
+            probe._set(k, v)
+        return dict(probe._p)
+
+    def _ratings(self, dataset, cols):
+        user = _checked_cast(_column(dataset, cols["userCol"]), cols["userCol"])
+        item = _checked_cast(_column(dataset, cols["itemCol"]), cols["itemCol"])
+        rating = np.ascontiguousarray(_column(dataset, cols["ratingCol"]), dtype=np.float32)
         if user.size == 0:
             raise IllegalArgumentException(_lib.ALS_E_INVALID_ARGUMENT,
                                            "No ratings available from the input dataset.")
+        return np.ascontiguousarray(user), np.ascontiguousarray(item), rating
+
+    def fit(self, dataset, params=None, initialUserFactors=None, initialItemFactors=None):
+        """ALS.fit (Spark Estimator.fit(dataset[, paramMap | paramMaps])).
+
+        `params` = one ParamMap (dict) -> one ALSModel fitted with those overrides; a list of ParamMaps
+        -> a list of ALSModels (the CV grid of ALSRecommenderCV.scala:67-90) that share ONE ingest
+        (id remap, both CSR orientations, shards) on the device: between fits only the
+        rank-dependent buffers are rebuilt (als_set_params).  The column names must agree across the
+        maps.  `initial*Factors` = (ids, factors[n, rank]) injects the start point (parity path, one
+        map only); without it the Spark-style XORShiftRandom initialisation is used."""
+        if isinstance(params, (list, tuple)):
+            return self._fit_many(dataset, [self._param_map(pm) for pm in params])
+        pm = self._param_map(params or {})
+        user, item, rating = self._ratings(dataset, pm)
         lib = load()
-        h = self._context()
+        h = self._context(pm)
         try:
-            user = np.ascontiguousarray(user)
-            item = np.ascontiguousarray(item)
             check(lib.als_set_ratings(h, user.size, ptr(user, C.c_int32), ptr(item, C.c_int32),
                                       ptr(rating, C.c_float)))
             for side, init in ((_lib.ALS_USER, initialUserFactors), (_lib.ALS_ITEM, initialItemFactors)):
@@ -170,9 +191,52 @@ class ALS(_Params):
         except Exception:
             lib.als_destroy(h)
             raise
-        model = ALSModel(h, dict(self._p))
+        model = ALSModel(h, pm)
         model.fit_seconds = fit_s
         return model
+
+    def _fit_many(self, dataset, maps):
+        if not maps:
+            return []
+        cols = ("userCol", "itemCol", "ratingCol")
+        if any(m[c] != maps[0][c] for m in maps for c in cols):
+            raise IllegalArgumentException(_lib.ALS_E_INVALID_ARGUMENT,
+                                           "a shared-ingest multi-fit needs the same columns in every ParamMap")
+        user, item, rating = self._ratings(dataset, maps[0])
+        lib = load()
+        h = self._context(maps[0])
+        models = []
+        try:
+            for pm in maps:  # validate every map before the ingest (no fit runs on a bad grid)
+                check(lib.als_set_params(h, C.byref(self._c_params(pm))))
+            check(lib.als_set_ratings(h, user.size, ptr(user, C.c_int32), ptr(item, C.c_int32),
+                                      ptr(rating, C.c_float)))
+            for pm in maps:
+                check(lib.als_set_params(h, C.byref(self._c_params(pm))))
+                t0 = time.perf_counter()
+                check(lib.als_fit(h))
+                fit_s = time.perf_counter() - t0
+                # snapshot the factors into a model-only context; the ingest context runs the next map
+                k = int(pm["rank"])
+                f = {}
+                for side in (_lib.ALS_USER, _lib.ALS_ITEM):
+                    n = lib.als_num_rows(h, side)
+                    ids = np.empty(n, dtype=np.int32)
+                    fac = np.empty((n, k), dtype=np.float32)
+                    check(lib.als_get_factors(h, side, ptr(ids, C.c_int32), ptr(fac, C.c_float)))
+                    f[side] = (ids, fac)
+                mh = C.c_void_p()
+                (ui, uf), (ii, itf) = f[_lib.ALS_USER], f[_lib.ALS_ITEM]
+                check(lib.als_model_create(k, ui.size, ptr(ui, C.c_int32), ptr(uf, C.c_float), ii.size,
+                                           ptr(ii, C.c_int32), ptr(itf, C.c_float), int(pm["device"]),
+                                           C.byref(mh)))
+                m = ALSModel(mh, pm)
+                m._cache.update(f)
+                m.fit_seconds = fit_s
+                models.append(m)
+        finally:
+            lib.als_destroy(h)
+        return models
 
 
 @_make_accessors

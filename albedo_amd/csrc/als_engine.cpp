@@ -205,6 +205,56 @@ inline int64_t padded_pos(const Side& S, int64_t i) {
   return r * S.maxrows + (i - S.starts[r]);
 }
 
+// Everything that depends on the rank / light-row limit rather than on the ratings: degree buckets
+// (the light limit follows KP), factor and rotated-factor buffers, Gram slabs.  Called after ingest
+// and again by als_set_params, so several fits (a CV grid) share one ingest.
+int rank_layout(als_ctx* c) {
+  const int64_t lmax = light_limit(c);
+  for (int side = 0; side < 2; ++side) {
+    Side& S = c->s[side];
+    // degree buckets (heavy rows longest first for the tail)
+    std::vector<int32_t> rows[NBUCKET];
+    for (int b = 0; b < NBUCKET; ++b) S.bnnz[b] = 0;
+    for (int64_t r = 0; r < S.own_n; ++r) {
+      const int b = bucket_of(S.h_deg[r], lmax);
+      rows[b].push_back((int32_t)r);
+      S.bnnz[b] += S.h_deg[r];
+    }
+    std::stable_sort(rows[B_HEAVY].begin(), rows[B_HEAVY].end(),
+                     [&](int32_t a, int32_t b) { return S.h_deg[a] > S.h_deg[b]; });
+    std::vector<int32_t> all;
+    all.reserve(S.own_n);
+    for (int b = 0; b < NBUCKET; ++b) {
+      S.boff[b] = (int64_t)all.size();
+      all.insert(all.end(), rows[b].begin(), rows[b].end());
+    }
+    S.boff[NBUCKET] = (int64_t)all.size();
+    HIPCHK(S.d_rows.ensure(all.size() * 4));
+    HIPCHK(hipMemcpy(S.d_rows.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
+  }
+  for (int side = 0; side < 2; ++side) {
+    Side& S = c->s[side];
+    HIPCHK(S.d_X.ensure((size_t)std::max<int64_t>(S.own_n, 1) * c->KP * 4));
+    HIPCHK(S.d_Z.ensure((size_t)std::max<int64_t>(c->world * S.maxrows, 1) * c->KP * 4));
+    HIPCHK(hipMemset(S.d_X.p, 0, S.d_X.bytes));
+    HIPCHK(hipMemset(S.d_Z.p, 0, S.d_Z.bytes));
+    S.B.assign((size_t)c->KP * c->KP, 0.0);
+    for (int i = 0; i < c->KP; ++i) S.B[(size_t)i * c->KP + i] = 1.0;
+    S.has_factors = false;
+    S.orig_valid = false;
+  }
+  const int64_t maxsrc = std::max(c->s[0].own_n, c->s[1].own_n);
+  c->slab_blocks = gram_slab_blocks(c->KP, maxsrc);
+  HIPCHK(c->slab.ensure(gram_slab_doubles(c->KP, c->slab_blocks) * 8));
+  HIPCHK(c->d_G.ensure((size_t)c->KP * c->KP * 8));
+  HIPCHK(c->d_P.ensure((size_t)c->KP * c->KP * 4));
+  HIPCHK(c->d_lam.ensure((size_t)c->KP * 4));
+  HIPCHK(c->d_err.ensure(16));
+  HIPCHK(c->d_cs.ensure((size_t)2 * c->KP * 4));
+  HIPCHK(c->d_csmax.ensure((size_t)c->KP * 4));
+  return ALS_OK;
+}
+
 // ---- ingest -------------------------------------------------------------------------------------
 int ingest_device(als_ctx* c, int64_t n, const int32_t* d_user, const int32_t* d_item, const float* d_rating) {
   if (n <= 0)
@@ -252,7 +302,6 @@ int ingest_device(als_ctx* c, int64_t n, const int32_t* d_user, const int32_t* d
   }
   ud.release();
   id.release();
-  const int64_t lmax = light_limit(c);
   for (int side = 0; side < 2; ++side) {
     Side& S = c->s[side];
     Side& Src = c->s[1 - side];
@@ -274,47 +323,10 @@ int ingest_device(als_ctx* c, int64_t n, const int32_t* d_user, const int32_t* d
       for (auto& v : hc) v = (int32_t)padded_pos(Src, v);
       HIPCHK(hipMemcpy(S.d_col.p, hc.data(), S.own_nnz * 4, hipMemcpyHostToDevice));
     }
-    // degree buckets (heavy rows longest first for the tail)
     S.h_deg.resize(S.own_n);
-    std::vector<int32_t> rows[NBUCKET];
-    for (int64_t r = 0; r < S.own_n; ++r) {
-      S.h_deg[r] = lp[r + 1] - lp[r];
-      const int b = bucket_of(S.h_deg[r], lmax);
-      rows[b].push_back((int32_t)r);
-      S.bnnz[b] += S.h_deg[r];
-    }
-    std::stable_sort(rows[B_HEAVY].begin(), rows[B_HEAVY].end(),
-                     [&](int32_t a, int32_t b) { return S.h_deg[a] > S.h_deg[b]; });
-    std::vector<int32_t> all;
-    all.reserve(S.own_n);
-    for (int b = 0; b < NBUCKET; ++b) {
-      S.boff[b] = (int64_t)all.size();
-      all.insert(all.end(), rows[b].begin(), rows[b].end());
-    }
-    S.boff[NBUCKET] = (int64_t)all.size();
-    HIPCHK(S.d_rows.ensure(all.size() * 4));
-    HIPCHK(hipMemcpy(S.d_rows.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
+    for (int64_t r = 0; r < S.own_n; ++r) S.h_deg[r] = lp[r + 1] - lp[r];
   }
-  for (int side = 0; side < 2; ++side) {
-    Side& S = c->s[side];
-    HIPCHK(S.d_X.ensure((size_t)std::max<int64_t>(S.own_n, 1) * c->KP * 4));
-    HIPCHK(S.d_Z.ensure((size_t)std::max<int64_t>(c->world * S.maxrows, 1) * c->KP * 4));
-    HIPCHK(hipMemset(S.d_X.p, 0, S.d_X.bytes));
-    HIPCHK(hipMemset(S.d_Z.p, 0, S.d_Z.bytes));
-    S.B.assign((size_t)c->KP * c->KP, 0.0);
-    for (int i = 0; i < c->KP; ++i) S.B[(size_t)i * c->KP + i] = 1.0;
-    S.has_factors = false;
-    S.orig_valid = false;
-  }
-  const int64_t maxsrc = std::max(c->s[0].own_n, c->s[1].own_n);
-  c->slab_blocks = gram_slab_blocks(c->KP, maxsrc);
-  HIPCHK(c->slab.ensure(gram_slab_doubles(c->KP, c->slab_blocks) * 8));
-  HIPCHK(c->d_G.ensure((size_t)c->KP * c->KP * 8));
-  HIPCHK(c->d_P.ensure((size_t)c->KP * c->KP * 4));
-  HIPCHK(c->d_lam.ensure((size_t)c->KP * 4));
-  HIPCHK(c->d_err.ensure(16));
-  HIPCHK(c->d_cs.ensure((size_t)2 * c->KP * 4));
-  HIPCHK(c->d_csmax.ensure((size_t)c->KP * 4));
+  TRYC(rank_layout(c));
   for (int side = 0; side < 2; ++side) {
     Side& S = c->s[side];
     unsigned bits = 0;
@@ -669,6 +681,19 @@ int als_create(const als_params* p, als_ctx** out) {
   *out = nullptr;
   TRYC(validate(p));
   return ctx_common(p, out);
+}
+
+int als_set_params(als_ctx* c, const als_params* p) {
+  if (!c || !p) return fail(ALS_E_INVALID_ARGUMENT, "null argument");
+  if (c->model_only) return fail(ALS_E_STATE, "als_set_params on a model-only context");
+  TRYC(validate(p));
+  TRYC(set_device(c));
+  const int dev = c->dev;
+  c->p = *p;
+  c->p.device = dev;  // the context stays on its device
+  c->KP = padded_rank(p->rank);
+  if (c->has_ratings) TRYC(rank_layout(c));  // factors are dropped: the next fit re-initialises
+  return ALS_OK;
 }
 
 void als_destroy(als_ctx* c) {

@@ -69,6 +69,11 @@ typedef struct als_ctx als_ctx;
 int als_params_default(als_params* p);
 int als_create(const als_params* p, als_ctx** out);
 void als_destroy(als_ctx* ctx);
+/* Replace the params of a context that already holds ratings (Spark Estimator.fit(dataset, paramMaps),
+ * ALSRecommenderCV.scala:67-90): the ingest (remap, both CSRs, shards) is kept, rank-dependent
+ * buffers and degree buckets are rebuilt and the factors are dropped, so the next als_fit starts
+ * from the new seed's initialisation.  Validated like als_create; the device is kept. */
+int als_set_params(als_ctx* ctx, const als_params* p);
 const char* als_last_error(void);
 int als_abi_version(void);
 /* number of visible gfx950 devices (0 when no GPU; never initialises a context) */

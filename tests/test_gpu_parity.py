@@ -248,6 +248,37 @@ def test_spark_init_on_device_matches_oracle(gpu_lib):
     assert np.array_equal(model.item_factors_np()[1], O.spark_initialize(B.item_ids, 7, si))
 
 
+def test_param_grid_fit_shares_ingest(gpu_lib):
+    """Estimator.fit(dataset, paramMaps) (the ALSRecommenderCV.scala:67-90 grid): one ingest, the
+    rank-dependent layout rebuilt per map (rank 8 -> 70 -> 8 crosses padded ranks 64/128, and the
+    light-row limit with them).  Each model equals its own standalone fit bit for bit, and the
+    first matches the fp64 oracle."""
+    from albedo_amd import ALS
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(900, 250, 12000, seed=36))
+    base = ALS(implicitPrefs=True, seed=42, maxIter=2)
+    grid = [dict(rank=8, regParam=0.5, alpha=40.0), dict(rank=70, regParam=0.1, alpha=10.0),
+            dict(rank=8, regParam=0.01, alpha=1.0, maxIter=3, seed=7)]
+    models = base.fit(d, grid)
+    assert len(models) == 3
+    for pm, m in zip(grid, models):
+        solo = ALS(**{**dict(implicitPrefs=True, seed=42, maxIter=2), **pm}).fit(d)
+        assert m.rank == pm["rank"] and m.getRegParam() == pm["regParam"]
+        for a, b in ((m.user_factors_np(), solo.user_factors_np()), (m.item_factors_np(), solo.item_factors_np())):
+            assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+        u = np.array([d["user"][0]], dtype=np.int32)
+        assert np.array_equal(m.recommend_np(5, subset=u)[1], solo.recommend_np(5, subset=u)[1])
+    B = O.make_blocks(d["user"], d["item"], d["rating"])
+    su, si = O.spark_side_seeds(42)
+    U, V = O.fit(B, rank=8, max_iter=2, reg=0.5, alpha=40.0, init_user=O.spark_initialize(B.user_ids, 8, su),
+                 init_item=O.spark_initialize(B.item_ids, 8, si))
+    assert _rel(models[0].user_factors_np()[1], U) < 1e-3
+    assert _rel(models[0].item_factors_np()[1], V) < 1e-3
+    # a single ParamMap overrides like Estimator.fit(dataset, paramMap)
+    one = base.fit(d, dict(rank=8, regParam=0.5, alpha=40.0))
+    assert np.array_equal(one.user_factors_np()[1], models[0].user_factors_np()[1])
+
+
 def test_facade_fit_matches_oracle_and_ndcg(gpu_lib):
     from albedo_amd import ALS
     from albedo_amd import evaluation as E

@@ -95,6 +95,13 @@ def test_param_validation_messages_without_gpu():
     with pytest.raises(IllegalArgumentException, match="No ratings"):
         ALS().fit({"user": np.array([], dtype=np.int32), "item": np.array([], dtype=np.int32),
                    "rating": np.array([], dtype=np.float32)})
+    d = {"user": np.array([1, 2]), "item": np.array([1, 1]), "rating": np.array([1.0, 1.0])}
+    with pytest.raises(IllegalArgumentException, match="rank given invalid value 0"):
+        ALS().fit(d, [dict(rank=0), dict(rank=4)])  # Estimator.fit(dataset, paramMaps)
+    with pytest.raises(IllegalArgumentException, match="unknown param"):
+        ALS().fit(d, dict(ranks=4))
+    with pytest.raises(IllegalArgumentException, match="same columns"):
+        ALS().fit(d, [dict(userCol="user"), dict(userCol="u")])
 
 
 def test_explain_params_and_setters():
