@@ -135,6 +135,8 @@ def main():
         tot_ms = stage[0][ti] + stage[1][ti]
         b = solve_bytes(0, which)[0] + solve_bytes(1, which)[0]
         kern[name] = dict(ms=tot_ms / args.steps, bytes_per_sweep=b)
+    if args.config in NONNEGATIVE:  # the explicit-solve timer holds solve_nnls_kernel (every row)
+        kern["solve_nnls"] = kern.pop("solve_heavy")
     dom = max(kern, key=lambda n: kern[n]["ms"])
     d = kern[dom]
     achieved = d["bytes_per_sweep"] / (d["ms"] / 1000.0) / 1e9 if d["ms"] > 0 else 0.0
