@@ -258,12 +258,13 @@ def test_param_grid_fit_shares_ingest(gpu_lib):
     d = generate(SynthSpec(900, 250, 12000, seed=36))
     base = ALS(implicitPrefs=True, seed=42, maxIter=2)
     grid = [dict(rank=8, regParam=0.5, alpha=40.0), dict(rank=70, regParam=0.1, alpha=10.0),
-            dict(rank=8, regParam=0.01, alpha=1.0, maxIter=3, seed=7)]
+            dict(rank=8, regParam=0.01, alpha=1.0, maxIter=3, seed=7), dict(rank=16, nonnegative=True)]
     models = base.fit(d, grid)
-    assert len(models) == 3
+    assert len(models) == 4
+    assert (models[3].user_factors_np()[1] >= 0).all() and (models[3].item_factors_np()[1] >= 0).all()
     for pm, m in zip(grid, models):
         solo = ALS(**{**dict(implicitPrefs=True, seed=42, maxIter=2), **pm}).fit(d)
-        assert m.rank == pm["rank"] and m.getRegParam() == pm["regParam"]
+        assert m.rank == pm["rank"] and m.getRegParam() == pm.get("regParam", base.getRegParam())
         for a, b in ((m.user_factors_np(), solo.user_factors_np()), (m.item_factors_np(), solo.item_factors_np())):
             assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
         u = np.array([d["user"][0]], dtype=np.int32)
