@@ -94,6 +94,7 @@ SIGNATURES = [
     ("als_run_sweeps", C.c_int, [P, C.c_int32]),
     ("als_half_sweep", C.c_int, [P, C.c_int]),
     ("als_get_gram", C.c_int, [P, C.c_int, F64P]),
+    ("als_get_degrees", C.c_int, [P, C.c_int, I64P]),
     ("als_get_row_ratings", C.c_int, [P, C.c_int, C.c_int32, C.c_int64, I32P, F32P, I64P]),
     ("als_model_create", C.c_int, [C.c_int32, C.c_int64, I32P, F32P, C.c_int64, I32P, F32P, C.c_int32, C.POINTER(P)]),
     ("als_recommend", C.c_int, [P, C.c_int, C.c_int32, I32P, C.c_int64, I32P, I32P, F32P]),

@@ -309,7 +309,9 @@ class ALSModel(_Params):
     def _recommend(self, side, num, subset=None):
         lib = load()
         if subset is not None:
-            sub = np.ascontiguousarray(np.unique(np.asarray(subset, dtype=np.int32)))
+            col = self._p["userCol"] if side == _lib.ALS_USER else self._p["itemCol"]
+            # checkedCast like fit/transform: out-of-Int-range or fractional ids raise, never wrap
+            sub = np.ascontiguousarray(np.unique(_checked_cast(subset, col)))
             nq = sub.size
         else:
             sub = None

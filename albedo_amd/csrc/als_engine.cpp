@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -96,12 +97,16 @@ struct Side {
   DevBuf d_X;                    // [own_n][KP] factors in basis B
   DevBuf d_Z;                    // [world*maxrows][KP] rotated factors (src role)
   std::vector<double> B;         // [KP][KP] basis: original = X · Bᵀ
-  std::vector<double> G;         // last Gram of this side (as src), [rank][rank]
+  std::vector<double> G;         // last Gram of this side (as src), [rank][rank], in basis GB
+  std::vector<double> GB;        // [KP][KP] the side's basis when G was computed (G_orig = GB G GBᵀ)
   bool has_factors = false;
   double t[ALS_T_COUNT] = {0};
   int64_t stats[4] = {0};
   DevBuf d_orig;                 // [n][KP] original-basis factors, dense order (materialised)
   bool orig_valid = false;
+  // split-K of the heavy tail: the first n_split heavy rows (degree > split chunk), their chunks
+  int64_t n_split = 0, n_chunks = 0;
+  DevBuf d_chunk_row, d_chunk_idx, d_slot0;
 };
 
 }  // namespace
@@ -122,6 +127,9 @@ struct als_ctx {
   bool has_ratings = false;
   bool model_only = false;
   DevBuf slab, d_G, d_P, d_lam, d_err, d_Gt, d_cs, d_csmax;
+  DevBuf d_partial, d_reduced;   // split-K partial / reduced A' records (shared by both sides)
+  int split_len = 0;             // ratings per split-K chunk (0: no split)
+  std::vector<float> h_P32, h_lam32, h_Gt;  // host staging of async H2D copies (outlive the sync)
   int slab_blocks = 0;
   hipEvent_t ev[8] = {};
 };
@@ -205,11 +213,23 @@ inline int64_t padded_pos(const Side& S, int64_t i) {
   return r * S.maxrows + (i - S.starts[r]);
 }
 
+// Ratings per split-K chunk.  A heavy row accumulates its A' in fp32 MFMA accumulators; beyond a
+// few hundred MFMA steps the accumulation error grows past the 1e-4 row tolerance (a 1.05M-star
+// row measured 4e-4) and one workgroup gathering a 10^6-star row is the launch's tail (45.9 ms for
+// 1.05M stars at rank 128).  8192 ratings = 256 MFMA steps per partial, summed in fp64.
+// ALBEDO_SPLIT_CHUNK overrides it for tuning (0 disables the split).
+int split_chunk_len() {
+  const char* e = std::getenv("ALBEDO_SPLIT_CHUNK");
+  if (e && *e) return std::max(0, std::atoi(e));
+  return 8192;
+}
+
 // Everything that depends on the rank / light-row limit rather than on the ratings: degree buckets
 // (the light limit follows KP), factor and rotated-factor buffers, Gram slabs.  Called after ingest
 // and again by als_set_params, so several fits (a CV grid) share one ingest.
 int rank_layout(als_ctx* c) {
   const int64_t lmax = light_limit(c);
+  c->split_len = split_chunk_len();
   for (int side = 0; side < 2; ++side) {
     Side& S = c->s[side];
     // degree buckets (heavy rows longest first for the tail)
@@ -231,6 +251,38 @@ int rank_layout(als_ctx* c) {
     S.boff[NBUCKET] = (int64_t)all.size();
     HIPCHK(S.d_rows.ensure(all.size() * 4));
     HIPCHK(hipMemcpy(S.d_rows.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
+    // split-K chunks of the heaviest rows (a prefix of the heavy list: sorted by degree)
+    const int64_t CH = c->split_len;
+    std::vector<int32_t> crow, cidx, slot0(1, 0);
+    S.n_split = 0;
+    for (int32_t r : rows[B_HEAVY]) {
+      if (CH <= 0 || S.h_deg[r] <= CH) break;
+      const int64_t nch = (S.h_deg[r] + CH - 1) / CH;
+      for (int64_t q = 0; q < nch; ++q) {
+        crow.push_back(r);
+        cidx.push_back((int32_t)q);
+      }
+      slot0.push_back((int32_t)crow.size());
+      ++S.n_split;
+    }
+    S.n_chunks = (int64_t)crow.size();
+    if (S.n_split > 0) {
+      HIPCHK(S.d_chunk_row.ensure(crow.size() * 4));
+      HIPCHK(S.d_chunk_idx.ensure(cidx.size() * 4));
+      HIPCHK(S.d_slot0.ensure(slot0.size() * 4));
+      HIPCHK(hipMemcpy(S.d_chunk_row.p, crow.data(), crow.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(S.d_chunk_idx.p, cidx.data(), cidx.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(S.d_slot0.p, slot0.data(), slot0.size() * 4, hipMemcpyHostToDevice));
+    }
+  }
+  {
+    const size_t rec = (size_t)split_rec_floats(c->KP) * 4;
+    const int64_t mc = std::max(c->s[0].n_chunks, c->s[1].n_chunks);
+    const int64_t ms = std::max(c->s[0].n_split, c->s[1].n_split);
+    if (mc > 0) {
+      HIPCHK(c->d_partial.ensure(mc * rec));
+      HIPCHK(c->d_reduced.ensure(ms * rec));
+    }
   }
   for (int side = 0; side < 2; ++side) {
     Side& S = c->s[side];
@@ -353,11 +405,15 @@ int upload_factors(als_ctx* c, int side, const float* f, int64_t ld) {
   return ALS_OK;
 }
 
+// Spark's initialize for every side that has no factors yet.  Both side seeds are always drawn
+// (seedGen.nextLong twice, user first), so a side initialised here gets the same rows whether or
+// not the other side was injected by the caller.
 int spark_init(als_ctx* c) {
   int64_t su, si;
   spark_side_seeds(c->p.seed, &su, &si);
   for (int side = 0; side < 2; ++side) {
     Side& S = c->s[side];
+    if (S.has_factors) continue;
     std::vector<float> f((size_t)S.n * c->p.rank);
     spark_initialize(S.ids.data(), S.n, c->p.rank, side == ALS_USER ? su : si,
                      side == ALS_USER ? c->p.num_user_blocks : c->p.num_item_blocks, f.data(), c->p.rank);
@@ -380,6 +436,8 @@ int column_scales(als_ctx* c, const Side& S, const Side& T) {
   return ALS_OK;
 }
 
+int heavy_launches(als_ctx* c, const Side& T, SolveArgs a, int64_t h0, int64_t hn, bool nnls);
+
 // nonnegative = true: Spark's NNLSSolver in the original basis (no rotation; B stays I)
 int half_sweep_nnls(als_ctx* c, int t) {
   const int sidx = 1 - t;
@@ -400,6 +458,7 @@ int half_sweep_nnls(als_ctx* c, int t) {
     S.G.assign((size_t)k * k, 0.0);
     for (int i = 0; i < k; ++i)
       for (int j = 0; j < k; ++j) S.G[(size_t)i * k + j] = Gf[(size_t)i * KP + j];
+    S.GB = S.B;
     for (int i = 0; i < KP; ++i)
       for (int j = 0; j <= i; ++j) gt[nnls_gtile_index(i, j)] = (float)Gf[(size_t)i * KP + j];
   }
@@ -428,9 +487,9 @@ int half_sweep_nnls(als_ctx* c, int t) {
   a.reg = (float)c->p.reg_param;
   a.err = c->d_err.as<int>();
   a.colscale = c->d_cs.as<float>();
-  a.rows = T.d_rows.as<int32_t>();
+  TRYC(heavy_launches(c, T, a, 0, T.boff[B_HEAVY], true));
+  TRYC(heavy_launches(c, T, a, T.boff[B_HEAVY], T.boff[NBUCKET] - T.boff[B_HEAVY], true));
   a.n_rows = T.boff[NBUCKET];
-  HIPCHK(launch_solve_nnls(KP, a, c->d_Gt.as<float>(), st));
   T.stats[0] = T.stats[1] = 0;
   T.stats[2] = a.n_rows;
   T.stats[3] = T.own_nnz;
@@ -449,6 +508,39 @@ int half_sweep_nnls(als_ctx* c, int t) {
   T.B = S.B;
   T.has_factors = true;
   T.orig_valid = false;
+  return ALS_OK;
+}
+
+// Heavy launch over rows [h0, h0 + hn) of T's bucket-ordered row list, the first T.n_split of which
+// (when h0 is the heavy bucket's start) are the split-K rows: chunk partials + fp64 reduce, then the
+// factor (or NNLS) from the reduced records, then the remaining rows as usual.
+int heavy_launches(als_ctx* c, const Side& T, SolveArgs a, int64_t h0, int64_t hn, bool nnls) {
+  const int KP = c->KP;
+  const int32_t* rows = T.d_rows.as<int32_t>();
+  int64_t ns = (h0 == T.boff[B_HEAVY]) ? std::min<int64_t>(T.n_split, hn) : 0;
+  if (ns > 0) {
+    SplitArgs sp{};
+    sp.chunk_row = T.d_chunk_row.as<int32_t>();
+    sp.chunk_idx = T.d_chunk_idx.as<int32_t>();
+    sp.n_chunks = T.n_chunks;
+    sp.chunk_len = c->split_len;
+    sp.slot0 = T.d_slot0.as<int32_t>();
+    sp.n_split = ns;
+    sp.partial = c->d_partial.as<float>();
+    sp.reduced = c->d_reduced.as<float>();
+    HIPCHK(launch_heavy_split(KP, a, sp, c->st));
+    SolveArgs b = a;
+    b.rows = rows + h0;
+    b.n_rows = ns;
+    b.prebuilt = c->d_reduced.as<float>();
+    if (nnls) HIPCHK(launch_solve_nnls(KP, b, c->d_Gt.as<float>(), c->st));
+    else HIPCHK(launch_solve_heavy(KP, b, c->st));
+  }
+  a.rows = rows + h0 + ns;
+  a.n_rows = hn - ns;
+  a.prebuilt = nullptr;
+  if (nnls) HIPCHK(launch_solve_nnls(KP, a, c->d_Gt.as<float>(), c->st));
+  else HIPCHK(launch_solve_heavy(KP, a, c->st));
   return ALS_OK;
 }
 
@@ -477,9 +569,14 @@ int half_sweep(als_ctx* c, int t) {
     for (int i = 0; i < k; ++i)
       for (int j = 0; j < k; ++j) Gk[(size_t)i * k + j] = Gf[(size_t)i * KP + j];
     S.G = Gk;
+    S.GB = S.B;
     if (!sym_eig(k, Gk.data(), w.data(), V.data()))
       return fail(ALS_E_NOT_POSITIVE_DEFINITE, "eigendecomposition of the Gram matrix did not converge");
-    std::vector<float> P32((size_t)KP * KP, 0.f), lam32(KP, 0.f);
+    // staging buffers live in the context: the async copies below read them after this block
+    std::vector<float>& P32 = c->h_P32;
+    std::vector<float>& lam32 = c->h_lam32;
+    P32.assign((size_t)KP * KP, 0.f);
+    lam32.assign(KP, 0.f);
     std::vector<double> Pf((size_t)KP * KP, 0.0);
     for (int i = 0; i < KP; ++i) Pf[(size_t)i * KP + i] = 1.0;
     for (int i = 0; i < k; ++i)
@@ -550,10 +647,8 @@ int half_sweep(als_ctx* c, int t) {
     T.stats[force_heavy ? 3 : 1] += T.bnnz[b];
   }
   HIPCHK(hipEventRecord(ev[5], st));
-  a.rows = rows + T.boff[B_HEAVY];
-  a.n_rows = T.boff[B_HEAVY + 1] - T.boff[B_HEAVY];
-  HIPCHK(launch_solve_heavy(KP, a, st));
-  T.stats[2] += a.n_rows;
+  TRYC(heavy_launches(c, T, a, T.boff[B_HEAVY], T.boff[B_HEAVY + 1] - T.boff[B_HEAVY], false));
+  T.stats[2] += T.boff[B_HEAVY + 1] - T.boff[B_HEAVY];
   T.stats[3] += T.bnnz[B_HEAVY];
   HIPCHK(hipEventRecord(ev[6], st));
   int err = 0;
@@ -798,6 +893,7 @@ int als_init_factors(als_ctx* c) {
   if (!c) return fail(ALS_E_INVALID_ARGUMENT, "null context");
   if (!c->has_ratings) return fail(ALS_E_STATE, "set ratings first");
   TRYC(set_device(c));
+  c->s[0].has_factors = c->s[1].has_factors = false;  // explicit request: both sides
   return spark_init(c);
 }
 
@@ -841,15 +937,31 @@ int als_fit(als_ctx* c) {
   if (!c->has_ratings)
     return fail(ALS_E_INVALID_ARGUMENT, "No ratings available from the input dataset (empty ratings).");
   TRYC(set_device(c));
-  if (!c->s[0].has_factors || !c->s[1].has_factors) TRYC(spark_init(c));
+  TRYC(spark_init(c));  // only the sides the caller did not inject
   return als_run_sweeps(c, c->p.max_iter);
 }
 
 int als_get_gram(als_ctx* c, int src_side, double* out) {
   if (!c || (src_side != 0 && src_side != 1) || !out) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
-  const auto& G = c->s[src_side].G;
+  const Side& S = c->s[src_side];
+  const auto& G = S.G;
   if (G.empty()) return fail(ALS_E_STATE, "no Gram computed yet");
-  std::memcpy(out, G.data(), G.size() * 8);
+  // G was formed from the factors in the side's basis at that time (original = X·GBᵀ):
+  // YᵀY = GB G GBᵀ, restricted to the model rank (GB is the identity on the padding)
+  const int k = c->p.rank, KP = c->KP;
+  std::vector<double> T((size_t)k * k, 0.0);  // T = GB_k G
+  for (int i = 0; i < k; ++i)
+    for (int m = 0; m < k; ++m) {
+      const double b = S.GB[(size_t)i * KP + m];
+      if (b == 0.0) continue;
+      for (int j = 0; j < k; ++j) T[(size_t)i * k + j] += b * G[(size_t)m * k + j];
+    }
+  for (int i = 0; i < k; ++i)
+    for (int j = 0; j < k; ++j) {
+      double acc = 0.0;
+      for (int m = 0; m < k; ++m) acc += T[(size_t)i * k + m] * S.GB[(size_t)j * KP + m];
+      out[(size_t)i * k + j] = acc;
+    }
   return ALS_OK;
 }
 
@@ -1078,6 +1190,15 @@ int als_get_row_ratings(als_ctx* c, int side, int32_t id, int64_t cap, int32_t* 
       const int64_t rk = Src.maxrows ? p / Src.maxrows : 0;
       src_ids[e] = Src.ids[Src.starts[rk] + (p - rk * Src.maxrows)];
     }
+  return ALS_OK;
+}
+
+int als_get_degrees(const als_ctx* c, int side, int64_t* out) {
+  if (!c || (side != 0 && side != 1) || !out) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  if (!c->has_ratings) return fail(ALS_E_STATE, "set ratings first");
+  const Side& S = c->s[side];
+  for (int64_t r = 0; r < S.n; ++r) out[r] = -1;
+  for (int64_t r = 0; r < S.own_n; ++r) out[S.own0 + r] = S.h_deg[r];
   return ALS_OK;
 }
 

@@ -858,6 +858,102 @@ __device__ __forceinline__ void heavy_build_all(const SolveArgs& a, int64_t p0, 
   __syncthreads();
 }
 
+// ---- split-K records (kernels.h SplitArgs): packed A' tiles | b' | positive-rating count ------
+template <int KP>
+struct SplitRec {
+  static constexpr int TILES = Heavy<KP>::NTL * HT_SZ;
+  static constexpr int OFF_B = TILES, OFF_N = OFF_B + KP;
+  static constexpr int FLOATS = (OFF_N + 1 + 3) & ~3;  // 16-B aligned records
+};
+int split_rec_floats(int KP) {
+  return KP == 64 ? SplitRec<64>::FLOATS : KP == 128 ? SplitRec<128>::FLOATS : SplitRec<256>::FLOATS;
+}
+
+// Element e of the packed lower tiles holds a matrix entry (not the pad column, not above the
+// diagonal of a diagonal tile): only those are written / summed, so stale stage bytes never travel.
+__device__ __forceinline__ bool tile_elem_valid(int e) {
+  const int t = e / HT_SZ, w = e - t * HT_SZ, r = w / HT_LD, c = w - r * HT_LD;
+  int I = (int)((sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  while (I * (I + 1) / 2 > t) --I;
+  const int J = t - I * (I + 1) / 2;
+  return c < 16 && (J < I || c <= r);
+}
+
+// Reduced record -> the LDS image heavy_build_all leaves behind (tiles at 0, b' at OFF_B, npos).
+template <int KP>
+__device__ __forceinline__ void heavy_load_record(const float* __restrict__ rec, float* smem) {
+  using H = Heavy<KP>;
+  using R = SplitRec<KP>;
+  for (int e = 4 * (int)threadIdx.x; e < R::TILES; e += 4 * H::NTH)
+    *reinterpret_cast<f32x4*>(smem + e) = ld4(rec + e);
+  for (int c = threadIdx.x; c < KP; c += H::NTH) smem[H::OFF_B + c] = rec[R::OFF_B + c];
+  if (threadIdx.x == 0) reinterpret_cast<int*>(smem + H::OFF_FLAG)[0] = reinterpret_cast<const int*>(rec)[R::OFF_N];
+  __syncthreads();
+}
+
+// One workgroup per chunk: the heavy build of chunk_len ratings of one row -> fp32 partial record.
+template <int KP>
+__global__ __launch_bounds__(Heavy<KP>::NTH, 4) void heavy_partial_kernel(SolveArgs a, SplitArgs s) {
+  using H = Heavy<KP>;
+  using R = SplitRec<KP>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  int* s_flag = reinterpret_cast<int*>(smem + H::OFF_FLAG);
+  const int tid = threadIdx.x;
+  const int64_t slot = blockIdx.x;
+  const int j = s.chunk_row[slot];
+  const int64_t rp0 = a.ptr[j], off = (int64_t)s.chunk_idx[slot] * s.chunk_len;
+  const int64_t rest = a.ptr[j + 1] - rp0 - off;
+  const int d = (int)(rest < s.chunk_len ? rest : s.chunk_len);  // >= 1: chunks cover the row
+  if (tid == 0) { s_flag[0] = 0; s_flag[1] = 0; }
+  heavy_build_all<KP>(a, rp0 + off, d, smem);
+  float* out = s.partial + slot * R::FLOATS;
+  for (int e = tid; e < R::TILES; e += H::NTH) out[e] = tile_elem_valid(e) ? smem[e] : 0.f;
+  for (int c = tid; c < KP; c += H::NTH) out[R::OFF_B + c] = smem[H::OFF_B + c];
+  if (tid == 0) reinterpret_cast<int*>(out)[R::OFF_N] = s_flag[0];
+}
+
+// Reduced record element e of split row r = Σ over the row's chunks (fp64, chunk order).
+template <int KP>
+__global__ __launch_bounds__(256) void heavy_reduce_kernel(SplitArgs s) {
+  using R = SplitRec<KP>;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e > R::OFF_N) return;
+  for (int64_t r = blockIdx.y; r < s.n_split; r += gridDim.y) {
+    const int q0 = s.slot0[r], q1 = s.slot0[r + 1];
+    float* out = s.reduced + r * R::FLOATS;
+    if (e == R::OFF_N) {
+      int n = 0;
+      for (int q = q0; q < q1; ++q) n += reinterpret_cast<const int*>(s.partial + (int64_t)q * R::FLOATS)[R::OFF_N];
+      reinterpret_cast<int*>(out)[R::OFF_N] = n;
+    } else {
+      double acc = 0.0;
+      for (int q = q0; q < q1; ++q) acc += (double)s.partial[(int64_t)q * R::FLOATS + e];
+      out[e] = (float)acc;
+    }
+  }
+}
+
+template <int KP>
+hipError_t launch_split_kp(const SolveArgs& a, const SplitArgs& s, hipStream_t st) {
+  using R = SplitRec<KP>;
+  const size_t lds = Heavy<KP>::FLOATS * 4;
+  static const hipError_t attr = allow_lds(heavy_partial_kernel<KP>, lds);
+  if (attr != hipSuccess) return attr;
+  heavy_partial_kernel<KP><<<(int)s.n_chunks, Heavy<KP>::NTH, lds, st>>>(a, s);
+  const int gy = (int)(s.n_split < 65535 ? s.n_split : 65535);
+  heavy_reduce_kernel<KP><<<dim3((R::OFF_N + 1 + 255) / 256, gy), 256, 0, st>>>(s);
+  return hipGetLastError();
+}
+
+hipError_t launch_heavy_split(int KP, const SolveArgs& a, const SplitArgs& s, hipStream_t st) {
+  if (s.n_chunks <= 0 || s.n_split <= 0) return hipSuccess;
+  if (KP == 64) return launch_split_kp<64>(a, s, st);
+  if (KP == 128) return launch_split_kp<128>(a, s, st);
+  if (KP == 256) return launch_split_kp<256>(a, s, st);
+  return hipErrorInvalidValue;
+}
+
 // 16x16 Cholesky of a diagonal tile in registers: lane i (of each 16-lane row) holds row i (rr[m],
 // m <= i meaningful).  On return rr[m] = L[i][m] (m <= i), dg = 1/L[i][i].  A pivot that collapses
 // below 2^-21 of its start value is numerically singular in fp32 (Spark's fp64 dppsv reports
@@ -883,7 +979,7 @@ __device__ __forceinline__ bool chol16(float (&rr)[16], float& dg, int i) {
 }
 
 // PH: phase mask for profiling probes (bit 0 build, bit 1 factor + substitution); the engine runs 3.
-template <int KP, int PH = 3>
+template <int KP, int PH = 3, bool PRE = false>
 __global__ __launch_bounds__(Heavy<KP>::NTH, 4) void solve_heavy_kernel(SolveArgs a) {
   using H = Heavy<KP>;
   constexpr int NB = KP / 16, NTH = H::NTH, NW = H::NW;
@@ -897,7 +993,9 @@ __global__ __launch_bounds__(Heavy<KP>::NTH, 4) void solve_heavy_kernel(SolveArg
   const int d = (int)(a.ptr[j + 1] - p0);
   if (tid == 0) { s_flag[0] = 0; s_flag[1] = 0; }
   HEAVY_TS(0);
-  if constexpr (PH & 1) {
+  if constexpr (PRE) {  // split row: A' / b' / npos reduced from the chunk partials
+    heavy_load_record<KP>(a.prebuilt + (size_t)blockIdx.x * SplitRec<KP>::FLOATS, smem);
+  } else if constexpr (PH & 1) {
     heavy_build_all<KP>(a, p0, d, smem);
   } else {
     for (int e = tid; e < H::OFF_DIAG; e += NTH) smem[e] = 0.f;
@@ -1122,7 +1220,7 @@ __device__ __forceinline__ bool nnls_stop(double step, double ndir, double nx) {
   return isnan(step) || step < 1e-7 || step > 1e40 || ndir < 1e-12 * nx || ndir < 1e-32;
 }
 
-template <int KP>
+template <int KP, bool PRE = false>
 __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a, const float* __restrict__ Gt) {
   using H = Heavy<KP>;
   using NL = NnlsLds<KP>;
@@ -1139,7 +1237,8 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
   const int64_t p0 = a.ptr[j];
   const int d = (int)(a.ptr[j + 1] - p0);
   if (tid == 0) { s_flag[0] = 0; s_flag[1] = 0; }
-  heavy_build_all<KP>(a, p0, d, smem);
+  if constexpr (PRE) heavy_load_record<KP>(a.prebuilt + (size_t)blockIdx.x * SplitRec<KP>::FLOATS, smem);
+  else heavy_build_all<KP>(a, p0, d, smem);
   const float lamn = a.reg * (float)(a.implicit ? s_flag[0] : d);
   for (int e = tid; e < NTL * HT_SZ; e += NTH) smem[e] += Gt[e];   // A = G + Σ c y yᵀ
   __syncthreads();
@@ -1220,9 +1319,12 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
 template <int KP>
 hipError_t launch_nnls_kp(const SolveArgs& a, const float* Gt, hipStream_t s) {
   const size_t lds = NnlsLds<KP>::FLOATS * 4;
-  static const hipError_t attr = allow_lds(solve_nnls_kernel<KP>, lds);
+  static const hipError_t attr = allow_lds(solve_nnls_kernel<KP, false>, lds);
+  static const hipError_t attr2 = allow_lds(solve_nnls_kernel<KP, true>, lds);
   if (attr != hipSuccess) return attr;
-  solve_nnls_kernel<KP><<<(int)a.n_rows, Heavy<KP>::NTH, lds, s>>>(a, Gt);
+  if (attr2 != hipSuccess) return attr2;
+  if (a.prebuilt) solve_nnls_kernel<KP, true><<<(int)a.n_rows, Heavy<KP>::NTH, lds, s>>>(a, Gt);
+  else solve_nnls_kernel<KP, false><<<(int)a.n_rows, Heavy<KP>::NTH, lds, s>>>(a, Gt);
   return hipGetLastError();
 }
 
@@ -1240,8 +1342,11 @@ template <int KP>
 hipError_t launch_heavy_kp(const SolveArgs& a, hipStream_t s) {
   const size_t lds = Heavy<KP>::FLOATS * 4;
   static const hipError_t attr = allow_lds(solve_heavy_kernel<KP>, lds);
+  static const hipError_t attr2 = allow_lds(solve_heavy_kernel<KP, 3, true>, lds);
   if (attr != hipSuccess) return attr;
-  solve_heavy_kernel<KP><<<(int)a.n_rows, Heavy<KP>::NTH, lds, s>>>(a);
+  if (attr2 != hipSuccess) return attr2;
+  if (a.prebuilt) solve_heavy_kernel<KP, 3, true><<<(int)a.n_rows, Heavy<KP>::NTH, lds, s>>>(a);
+  else solve_heavy_kernel<KP><<<(int)a.n_rows, Heavy<KP>::NTH, lds, s>>>(a);
   return hipGetLastError();
 }
 

@@ -24,7 +24,26 @@ struct SolveArgs {
   float reg;
   int* err;                // device flag: set to 1 when a solve meets a non-positive pivot
   const float* colscale;   // [2*KP] heavy-build fp16 column scales 2^e and their inverses
+  const float* prebuilt;   // split rows: reduced A' records [n_rows][split_rec_floats] (else null)
 };
+
+// Split-K of the heavy tail (rows with more ratings than one chunk): every chunk of chunk_len
+// ratings is built by its own workgroup into an fp32 partial record (packed A' tiles + b' + the
+// positive-rating count), the partials of a row are summed in fp64 in chunk order (deterministic),
+// and the row is factored from the reduced record (SolveArgs::prebuilt).
+struct SplitArgs {
+  const int32_t* chunk_row;  // [n_chunks] dst row (CSR row index) of each chunk
+  const int32_t* chunk_idx;  // [n_chunks] chunk number within its row
+  int64_t n_chunks;
+  int chunk_len;
+  const int32_t* slot0;      // [n_split + 1] first chunk of each split row (rows in factor order)
+  int64_t n_split;
+  float* partial;            // [n_chunks][split_rec_floats]
+  float* reduced;            // [n_split][split_rec_floats]
+};
+int split_rec_floats(int KP);
+// partial builds of every chunk, then the fp64 reduction into s.reduced
+hipError_t launch_heavy_split(int KP, const SolveArgs& a, const SplitArgs& s, hipStream_t st);
 
 // G (fp64 [KP][KP], full symmetric) = Σ_rows Xᵀ X over rows [0, n) of X ([n][KP]).
 hipError_t launch_gram(int KP, const float* X, int64_t n, double* slab, int slab_blocks, double* G,

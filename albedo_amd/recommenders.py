@@ -26,7 +26,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import IllegalArgumentException
-from .als import ALSModel
+from .als import ALSModel, _checked_cast
 from . import settings
 
 _SPARK_TYPES = {"i4": "IntegerType", "i8": "LongType", "i2": "ShortType", "i1": "ByteType",
@@ -113,7 +113,7 @@ class ALSRecommender(Recommender):
         model = self.alsModel
         uids, _ = model.user_factors_np()
         # activeUsers ⋈ userFactors on id (ALSRecommender.scala:33-34): unknown users drop out
-        active = np.intersect1d(np.asarray(users, dtype=np.int32), uids)
+        active = np.intersect1d(_checked_cast(users, self._p["userCol"]), uids)
         num = int(self._p["topK"])
         if active.size == 0 or num <= 0:
             return np.empty(0, np.int32), np.empty(0, np.int32), np.empty(0, np.float32)

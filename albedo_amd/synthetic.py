@@ -5,7 +5,8 @@ The reference trains on the `app_repostarring` table (`DatasetUtils.scala:111-12
 (`DatasetUtils.scala:118`).  That dump is not available offline, so every config is
 a synthetic stand-in with the shape SURVEY.md §8(d) fixes:
 
-* repo popularity  w_j ∝ (j+1)^-s  over a seeded shuffle of repo positions;
+* repo popularity  w_j ∝ (j+1)^-s  over a seeded shuffle of repo positions (optionally a "head":
+  fixed draw probabilities for the top ranks, config c5's >1M-star repos);
 * user degree      P(d) ∝ d^-1.8 on [1, min(dmax, I)], rescaled to exactly N nonzeros;
 * per-user draws without replacement (duplicates are re-drawn, `rounds` times at most);
 * sparse Int ids through an odd-multiplier bijection of [0, 2^31) so the engine's id remap is
@@ -74,6 +75,7 @@ class SynthSpec:
     dmax: int = 20000
     seed: int = 42
     rounds: int = 8
+    head: tuple = ()  # draw probabilities of the top popularity ranks (the rest: Zipf body)
 
     def degree_cap(self) -> int:
         # keep every user at most half the catalogue so draws without replacement converge
@@ -85,7 +87,10 @@ CONFIGS = {
     "c1p": SynthSpec(1_000_000, 200_000, 50_000_000, zipf_s=0.7),
     "c2": SynthSpec(1_000_000, 200_000, 50_000_000, zipf_s=0.7),
     "c4": SynthSpec(20_000_000, 4_000_000, 1_000_000_000, zipf_s=0.8),
-    "c5": SynthSpec(5_000_000, 500_000, 100_000_000, zipf_s=0.9),
+    # config 5 asks for "extreme degree skew (top repos >1M stars)": a Zipf(0.9) body alone tops
+    # out at ~0.79M stars (most users star 1-2 repos, so a repo's reach saturates), so the three
+    # most popular repos take 12 % / 9 % / 7 % of the draws: ~1.7M / 1.4M / 1.2M stars
+    "c5": SynthSpec(5_000_000, 500_000, 100_000_000, zipf_s=0.9, head=(0.12, 0.09, 0.07)),
 }
 
 
@@ -123,6 +128,10 @@ def popularity_table(spec: SynthSpec):
     """(cumulative weights over popularity rank, rank -> repo position permutation)."""
     I = spec.n_items
     w = (np.arange(1, I + 1, dtype=np.float64)) ** (-spec.zipf_s)
+    if spec.head:
+        h = np.asarray(spec.head, dtype=np.float64)
+        w *= (1.0 - h.sum()) / w.sum()
+        w[: h.size] += h
     cw = np.cumsum(w)
     perm = np.random.Generator(np.random.PCG64(spec.seed)).permutation(I).astype(np.int32)
     return cw, perm

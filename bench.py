@@ -13,7 +13,8 @@ roofline: the dominant per-row solve kernel's algorithmic bytes per launch (SURV
   nnz·(4 col + 4 val) + (rows+1)·8 + nnz·4k gathered rows + rows·4k written) / its average
   HIP-event duration on the engine's stream, against 8 TB/s HBM.
 cpu_baseline: the fp64 C/OpenMP restatement of Spark's half-sweep (oracle/c, "port") timed on a
-  bounded row sample of the same workload on this host, extrapolated to one sweep.
+  degree-stratified row sample of the same workload on every core this process may use (affinity /
+  cgroup quota; nproc and the CPU model are reported), each stratum extrapolated to one sweep.
 """
 from __future__ import annotations
 
@@ -91,6 +92,11 @@ def main():
     setup_s = time.perf_counter() - t0
     nnz = lib.als_num_ratings(h)
     n_users, n_items = lib.als_num_rows(h, 0), lib.als_num_rows(h, 1)
+    top_deg = {}
+    for side, name in ((0, "users"), (1, "repos")):
+        dg = np.empty(lib.als_num_rows(h, side), np.int64)
+        L.check(lib.als_get_degrees(h, side, L.ptr(dg, C.c_int64)))
+        top_deg[name] = np.sort(dg[dg >= 0])[::-1][:5].tolist()
 
     def barrier():
         L.check(lib.als_synchronize(h))
@@ -173,11 +179,14 @@ def main():
         line = {
             "metric": METRIC, "value": value, "unit": "interactions/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "fp32 (split-fp16x3 MFMA build, fp32 accumulate; fp64 Gram/eigenbasis"
+                     + ("; fp64 NNLS vectors)" if args.config in NONNEGATIVE else ")"),
             "data": "synthetic (seeded power-law star matrix, rating=1.0; SURVEY.md §8(d))",
             "config": {"workload": f"BASELINE {args.config}: {n_users} users x {n_items} repos, {nnz} stars, "
                                    f"rank {k}, implicit alpha 40 regParam 0.5, one sweep = item + user half",
-                       "rank": k, "nnz": int(nnz), "parallelism": f"row-shard x{world} (RCCL)"},
+                       "rank": k, "nnz": int(nnz), "parallelism": f"row-shard x{world} (RCCL)",
+                       "nonnegative": args.config in NONNEGATIVE, "top5_degrees": top_deg},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                          "frac": achieved / peak, "traffic": traffic, "kernel": dom,
                          "traffic_unit": "GB per sweep (PMC, profiles/pmc_traffic_<config>.json)",
@@ -196,11 +205,44 @@ def main():
         dist.destroy_process_group()
 
 
+def host_cpu_info():
+    """Cores this process may use (affinity, cgroup quota), the machine's nproc and CPU model."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = min(aff, quota) if quota else aff
+    return dict(nproc=nproc, affinity=aff, cgroup_quota=quota, model=model, usable=usable)
+
+
+# degree strata of the CPU sample (per-star cost differs between a 2-star and a 10^5-star row)
+STRATA = (1, 17, 33, 65, 257, 1025, 4097, 16385, 65537)
+
+
 def cpu_baseline(lib, L, h, k, nnz, n_users, n_items, budget_s):
-    """fp64 C/OpenMP restatement (oracle/c) on a bounded sample of this workload's rows."""
+    """fp64 C/OpenMP restatement (oracle/c) timed on a degree-stratified sample of this workload's
+    rows, on every core this process may use; each stratum is extrapolated by its own star count."""
     from oracle import cbind
-    threads = min(16, os.cpu_count() or 1)
+    info = host_cpu_info()
+    threads = info["usable"]
     res = {}
+    t_sweep = 0.0
     for dst, n_dst, n_src in ((0, n_users, n_items), (1, n_items, n_users)):
         src = 1 - dst
         sids = np.empty(n_src, np.int32)
@@ -211,46 +253,65 @@ def cpu_baseline(lib, L, h, k, nnz, n_users, n_items, budget_s):
         g_s = time.perf_counter() - t0
         dids = np.empty(n_dst, np.int32)
         L.check(lib.als_get_ids(h, dst, L.ptr(dids, C.c_int32)))
+        deg = np.empty(n_dst, np.int64)
+        L.check(lib.als_get_degrees(h, dst, L.ptr(deg, C.c_int64)))
         rng = np.random.default_rng(7 + dst)
-        order = rng.permutation(n_dst)
-        ptr, cols, vals = [0], [], []
+        edges = list(STRATA) + [int(deg.max()) + 1]
+        n_b = sum(1 for a, b in zip(edges[:-1], edges[1:]) if np.any((deg >= a) & (deg < b)))
+        per_star = None  # seconds per star of the last measured stratum (for strata past the cap)
+        strata = []
+        t_side = g_s
         n_row = np.empty(1, np.int64)
-        buf_i, buf_v = np.empty(1 << 16, np.int32), np.empty(1 << 16, np.float32)
-        total = 0
-        t_rows = 0.0
-        done = 0
-        chunk = 256
-        while done < n_dst and t_rows < budget_s / 2:
-            sel = order[done:done + chunk]
-            done += len(sel)
-            ptr, cols, vals = [0], [], []
-            for r in sel:
-                L.check(lib.als_get_row_ratings(h, dst, int(dids[r]), buf_i.size, L.ptr(buf_i, C.c_int32),
-                                                L.ptr(buf_v, C.c_float), L.ptr(n_row, C.c_int64)))
-                m = int(n_row[0])
-                if m > buf_i.size:  # row larger than the buffer: grow once and fetch again
-                    buf_i, buf_v = np.empty(m, np.int32), np.empty(m, np.float32)
-                    L.check(lib.als_get_row_ratings(h, dst, int(dids[r]), m, L.ptr(buf_i, C.c_int32),
-                                                    L.ptr(buf_v, C.c_float), L.ptr(n_row, C.c_int64)))
-                cols.append(np.searchsorted(sids, buf_i[:m]).astype(np.int32))
-                vals.append(buf_v[:m].copy())
-                ptr.append(ptr[-1] + m)
-            ptr_a = np.asarray(ptr, np.int64)
-            t1 = time.perf_counter()
-            cbind.solve_rows(sf, G, ptr_a, np.concatenate(cols), np.concatenate(vals), reg=0.5, alpha=40.0,
-                             implicit=True, threads=threads)
-            t_rows += time.perf_counter() - t1
-            total += int(ptr_a[-1])
-            chunk = min(chunk * 2, 8192)
-        res[dst] = dict(gram_s=g_s, rows_s=t_rows, sample_nnz=total, sample_rows=done)
+        for a, b in zip(edges[:-1], edges[1:]):
+            rows = np.nonzero((deg >= a) & (deg < b))[0]
+            if rows.size == 0:
+                continue
+            stars = int(deg[rows].sum())
+            if a >= STRATA[-1] and per_star is not None:
+                # single rows of 10^5+ stars would run on one core for minutes: the build is one dspr
+                # per star in every stratum, so the per-star cost of the 16K-65K stratum is used
+                strata.append(dict(lo=a, rows=int(rows.size), stars=stars, sampled_rows=0, sampled_stars=0,
+                                   s=per_star * stars, extrapolated_from_lower=True))
+                t_side += per_star * stars
+                continue
+            order = rng.permutation(rows)
+            done, t_rows, total = 0, 0.0, 0
+            chunk = max(2 * threads, 64)
+            while done < order.size and (t_rows < budget_s / (2 * n_b) or done == 0):
+                sel = order[done:done + chunk]
+                done += sel.size
+                ptr, cols, vals = [0], [], []
+                for r in sel:
+                    m = int(deg[r])
+                    bi, bv = np.empty(max(m, 1), np.int32), np.empty(max(m, 1), np.float32)
+                    L.check(lib.als_get_row_ratings(h, dst, int(dids[r]), m, L.ptr(bi, C.c_int32),
+                                                    L.ptr(bv, C.c_float), L.ptr(n_row, C.c_int64)))
+                    cols.append(np.searchsorted(sids, bi[:m]).astype(np.int32))
+                    vals.append(bv[:m])
+                    ptr.append(ptr[-1] + m)
+                ptr_a = np.asarray(ptr, np.int64)
+                t1 = time.perf_counter()
+                cbind.solve_rows(sf, G, ptr_a, np.concatenate(cols), np.concatenate(vals), reg=0.5, alpha=40.0,
+                                 implicit=True, threads=threads)
+                t_rows += time.perf_counter() - t1
+                total += int(ptr_a[-1])
+                chunk = min(chunk * 2, 8192)
+            per_star = t_rows / max(total, 1)
+            est = t_rows * stars / max(total, 1)
+            strata.append(dict(lo=a, rows=int(rows.size), stars=stars, sampled_rows=int(done), sampled_stars=total,
+                               s=est))
+            t_side += est
+        res[dst] = dict(gram_s=g_s, strata=strata, side_s=t_side)
+        t_sweep += t_side
         del sf
-    # extrapolate one sweep: Gram of each src side + per-nnz row cost over all stars
-    t_sweep = sum(res[d]["gram_s"] + res[d]["rows_s"] * (nnz / max(res[d]["sample_nnz"], 1)) for d in res)
+    sampled = sum(st["sampled_stars"] for d in res for st in res[d]["strata"])
     return {"value": nnz / t_sweep, "unit": "interactions/s", "cores": threads, "kind": "port",
-            "sample": (f"fp64 C/OpenMP restatement of Spark's half-sweep (oracle/c/als_cpu.c): full Gram of each src "
-                       f"side + {res[0]['sample_rows']} user rows ({res[0]['sample_nnz']} stars) and "
-                       f"{res[1]['sample_rows']} repo rows ({res[1]['sample_nnz']} stars) solved, extrapolated "
-                       f"per star to one full sweep")}
+            "host": {k2: info[k2] for k2 in ("nproc", "affinity", "cgroup_quota", "model")},
+            "sweep_s_extrapolated": t_sweep,
+            "strata": {("user" if d == 0 else "item"): res[d]["strata"] for d in res},
+            "sample": (f"fp64 C/OpenMP restatement of Spark's half-sweep (oracle/c/als_cpu.c, {threads} threads): "
+                       f"full Gram of each src side + a degree-stratified row sample ({sampled} stars, strata "
+                       f"{list(STRATA)}) solved, each stratum extrapolated by its own star count to one sweep")}
 
 
 if __name__ == "__main__":

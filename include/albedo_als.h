@@ -117,7 +117,11 @@ int als_half_sweep(als_ctx* ctx, int dst_side);
  * are filled only when n_out <= cap.  Rows of other ranks are not available (ALS_E_STATE). */
 int als_get_row_ratings(als_ctx* ctx, int side, int32_t id, int64_t cap, int32_t* src_ids, float* ratings,
                         int64_t* n_out);
-/* Debug/parity: fetch the last Gram matrix of `src_side` (fp64, [rank][rank]). */
+/* Ratings per row of `side` in ascending id order (this rank's rows; -1 for rows other ranks own).
+ * Observability for the power-law skew (the per-row work of Spark's computeFactors). */
+int als_get_degrees(const als_ctx* ctx, int side, int64_t* out);
+/* Debug/parity: the last Gram matrix YᵀY of `src_side` in the original basis (fp64, [rank][rank];
+ * Spark computeYtY of the src factors the last half-sweep solved from). */
 int als_get_gram(als_ctx* ctx, int src_side, double* out);
 
 /* ---- model (ALSModel) ------------------------------------------------------------------------ */

@@ -446,10 +446,38 @@ def test_device_synthetic_generator_matches_numpy(gpu_lib):
     assert np.array_equal(u[:m], ref["user"]) and np.array_equal(i[:m], ref["item"])
 
 
+def _check_rows_fp64(gpu_lib, c, side, rows_ids, X_ids, X, Y_ids, Y, k):
+    """Rows `rows_ids` of `side` (solved into X) equal the fp64 solve of Spark's implicit normal
+    equation from the src factors Y, built from the engine's own CSR; returns the worst error."""
+    from albedo_amd import _lib as L
+    Y64 = Y.astype(np.float64)
+    G = Y64.T @ Y64
+    n_row = np.empty(1, np.int64)
+    worst = 0.0
+    for rid in rows_ids:
+        L.check(gpu_lib.als_get_row_ratings(c.h, side, int(rid), 0, None, None, L.ptr(n_row, C.c_int64)))
+        cap = int(n_row[0])
+        src = np.empty(max(cap, 1), np.int32)
+        rat = np.empty(max(cap, 1), np.float32)
+        L.check(gpu_lib.als_get_row_ratings(c.h, side, int(rid), cap, L.ptr(src, C.c_int32), L.ptr(rat, C.c_float),
+                                            L.ptr(n_row, C.c_int64)))
+        n = int(n_row[0])
+        Yr = Y64[np.searchsorted(Y_ids, src[:n])]
+        cvec = 40.0 * np.abs(rat[:n].astype(np.float64))
+        A = G + (Yr.T * cvec) @ Yr + 0.5 * np.sum(rat[:n] > 0) * np.eye(k)
+        b = Yr.T @ np.where(rat[:n] > 0, 1.0 + cvec, 0.0)
+        x = np.linalg.solve(A, b)
+        err = np.max(np.abs(X[np.searchsorted(X_ids, rid)] - x)) / np.max(np.abs(x))
+        assert err < 1e-4, f"side {side} id {rid} ({n} ratings): rel err {err:.3e}"
+        worst = max(worst, float(err))
+    return worst
+
+
 def test_c2_scale_rows_match_fp64_solve(gpu_lib):
     """Full-size property at BASELINE config 2 (1M x 200k, 50M nnz, rank 64): after an item and a
-    user half-sweep from Spark-style init, sampled rows of every degree bucket equal the fp64
-    solution of Spark's normal equation built on the host from the engine's own inputs."""
+    user half-sweep from Spark-style init, sampled rows of every degree bucket -- and the 10 most
+    starred repos (the power-law tail, 10^5 stars) -- equal the fp64 solution of Spark's normal
+    equation built on the host from the engine's own inputs."""
     from albedo_amd import _lib as L
     from albedo_amd.synthetic import CONFIGS, popularity_table, user_degrees
     spec = CONFIGS["c2"]
@@ -462,32 +490,21 @@ def test_c2_scale_rows_match_fp64_solve(gpu_lib):
                                               L.ptr(np.ascontiguousarray(perm), C.c_int32)))
     assert gpu_lib.als_num_ratings(c.h) > 0.99 * spec.nnz
     L.check(gpu_lib.als_init_factors(c.h))
+    uids, U0 = c.factors(0)
     c.half(1)
+    iids, V = c.factors(1)
+    deg = np.empty(iids.size, np.int64)
+    L.check(gpu_lib.als_get_degrees(c.h, 1, L.ptr(deg, C.c_int64)))
+    top = iids[np.argsort(-deg, kind="stable")[:10]]
+    assert deg.max() > 100_000  # the tail this arm is about
+    rng = np.random.default_rng(1)
+    _check_rows_fp64(gpu_lib, c, 1, np.r_[top, rng.choice(iids, 100, replace=False)], iids, V, uids, U0, 64)
     c.half(0)
     st = c.stats(0)
     assert st[0] > 0 and st[2] > 0  # both solve paths ran
-    uids, U = c.factors(0)
-    iids, V = c.factors(1)
-    V64 = V.astype(np.float64)
-    G = V64.T @ V64
+    _, U = c.factors(0)
     rng = np.random.default_rng(0)
-    n_row = np.empty(1, np.int64)
-    checked = 0
-    for r in rng.choice(len(uids), 200, replace=False):
-        cap = 50000
-        src = np.empty(cap, np.int32)
-        rat = np.empty(cap, np.float32)
-        L.check(gpu_lib.als_get_row_ratings(c.h, 0, int(uids[r]), cap, L.ptr(src, C.c_int32), L.ptr(rat, C.c_float),
-                                            L.ptr(n_row, C.c_int64)))
-        n = int(n_row[0])
-        Y = V64[np.searchsorted(iids, src[:n])]
-        cvec = 40.0 * np.abs(rat[:n].astype(np.float64))
-        A = G + (Y.T * cvec) @ Y + 0.5 * np.sum(rat[:n] > 0) * np.eye(64)
-        b = Y.T @ np.where(rat[:n] > 0, 1.0 + cvec, 0.0)
-        x = np.linalg.solve(A, b)
-        assert np.max(np.abs(U[r] - x)) / np.max(np.abs(x)) < 1e-4
-        checked += 1
-    assert checked == 200
+    _check_rows_fp64(gpu_lib, c, 0, uids[rng.choice(len(uids), 200, replace=False)], uids, U, iids, V, 64)
 
 
 # ---- NNLS (nonnegative = true) --------------------------------------------------------------
