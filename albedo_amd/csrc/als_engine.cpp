@@ -218,6 +218,10 @@ inline int64_t padded_pos(const Side& S, int64_t i) {
 // row measured 4e-4) and one workgroup gathering a 10^6-star row is the launch's tail (45.9 ms for
 // 1.05M stars at rank 128).  8192 ratings = 256 MFMA steps per partial, summed in fp64.
 // ALBEDO_SPLIT_CHUNK overrides it for tuning (0 disables the split).
+// Heavy rows at padded rank <= 128 run one wave per row (heavy_wave.hip) unless ALBEDO_HEAVY=wg
+// selects the 4-wave workgroup kernel (A/B measurements); rank 256 always uses the workgroup kernel.
+bool use_wave_kernel(const als_ctx* c);
+
 int split_chunk_len() {
   const char* e = std::getenv("ALBEDO_SPLIT_CHUNK");
   if (e && *e) return std::max(0, std::atoi(e));
@@ -540,8 +544,17 @@ int heavy_launches(als_ctx* c, const Side& T, SolveArgs a, int64_t h0, int64_t h
   a.n_rows = hn - ns;
   a.prebuilt = nullptr;
   if (nnls) HIPCHK(launch_solve_nnls(KP, a, c->d_Gt.as<float>(), c->st));
+  else if (use_wave_kernel(c)) HIPCHK(launch_solve_wave(KP, a, c->st));
   else HIPCHK(launch_solve_heavy(KP, a, c->st));
   return ALS_OK;
+}
+
+bool use_wave_kernel(const als_ctx* c) {
+  static const bool wg = [] {
+    const char* e = std::getenv("ALBEDO_HEAVY");
+    return e && std::strcmp(e, "wg") == 0;
+  }();
+  return c->KP <= 128 && !wg;
 }
 
 int half_sweep(als_ctx* c, int t) {
@@ -641,7 +654,8 @@ int half_sweep(als_ctx* c, int t) {
   for (int b = 0; b < 3; ++b) {
     a.rows = rows + T.boff[b];
     a.n_rows = T.boff[b + 1] - T.boff[b];
-    if (force_heavy) HIPCHK(launch_solve_heavy(KP, a, st));
+    if (force_heavy && use_wave_kernel(c)) HIPCHK(launch_solve_wave(KP, a, st));
+    else if (force_heavy) HIPCHK(launch_solve_heavy(KP, a, st));
     else HIPCHK(launch_solve_light(KP, Dof[b], a, st));
     T.stats[force_heavy ? 2 : 0] += a.n_rows;
     T.stats[force_heavy ? 3 : 1] += T.bnnz[b];

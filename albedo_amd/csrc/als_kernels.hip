@@ -22,6 +22,7 @@
 #include <type_traits>
 #include <utility>
 #include "kernels.h"
+#include "device_common.h"
 
 namespace albedo {
 
@@ -32,98 +33,6 @@ __device__ unsigned long long albedo_heavy_ts[64][48];
 #else
 #define HEAVY_TS(k)
 #endif
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-#define WAVE_LDS_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
-
-__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ float rdlane(float x, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
-}
-__device__ __forceinline__ int rdlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
-// Broadcast of lane M of every 16-lane row to the whole row (DPP row_newbcast, gfx90a+): the
-// diagonal-block kernels below keep one 16x16 problem per 16-lane row (rows replicated), so a
-// broadcast is one v_mov_dpp instead of a v_readlane + SGPR hazard.
-template <int M>
-__device__ __forceinline__ float bc16(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + M, 0xF, 0xF, true));
-}
-
-// acc -= (v of lane M of the 16-lane row) * w in ONE instruction (v_fmac_f32 with a DPP
-// row_newbcast source; the compiler keeps the broadcast as a separate v_mov_b32_dpp).  Same single
-// rounding as fmaf(-w, bc16<M>(v), acc).  NOP: v may have been written by the previous VALU
-// instruction (a DPP source needs 2 wait states, which the compiler does not insert around asm);
-// volatile keeps these in program order, so only the first use after a write needs it.
-template <int M, bool NOP>
-__device__ __forceinline__ void fnmac_bc16(float& acc, float v, float w) {
-  if constexpr (NOP)
-    asm volatile("s_nop 1\n\tv_fmac_f32_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-                 : "+v"(acc) : "v"(v), "v"(w), "n"(M));
-  else
-    asm volatile("v_fmac_f32_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-                 : "+v"(acc) : "v"(v), "v"(w), "n"(M));
-}
-// bc16 for a source written by asm (fnmac_bc16): the wait states are explicit
-template <int M>
-__device__ __forceinline__ float bc16_after_asm(float v) {
-  float r;
-  asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-               : "=v"(r) : "v"(v), "n"(M));
-  return r;
-}
-
-// Sum over each 16-lane row, result in the row's lane 15: DPP row_shr prefix sums (VALU only; a
-// __shfl_xor butterfly goes through the LDS crossbar instead).
-__device__ __forceinline__ float sum16_last(float x) {
-  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x111, 0xF, 0xF, true));  // row_shr:1
-  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x112, 0xF, 0xF, true));  // row_shr:2
-  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x114, 0xF, 0xF, true));  // row_shr:4
-  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x118, 0xF, 0xF, true));  // row_shr:8
-  return x;
-}
-
-// v_rsq_f32 / v_rcp_f32 / v_sqrt_f32: single instructions (~1 ulp) instead of the IEEE-exact
-// multi-instruction expansions; the solve tolerance is 1e-4 relative (tests state it)
-__device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
-__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
-__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ f32x4 mfma_h(f16x8 a, f16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
-
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N>(f);
-  }
-}
-
-// Dynamic LDS beyond 64 KiB needs the per-kernel attribute (set once per instantiation).
-template <typename K>
-hipError_t allow_lds(K kernel, size_t bytes) {
-  if (bytes <= 65536) return hipSuccess;
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)bytes);
-}
-
-struct TilePair { int a, b; };
-// t-th tile of the upper triangle (a <= b) of an nq x nq block grid, row-major.
-__host__ __device__ constexpr TilePair upper_tile(int t, int nq) {
-  int a = 0;
-  while (t >= nq - a) { t -= nq - a; ++a; }
-  return TilePair{a, a + t};
-}
-// Column of local index i in permuted 16-column block q (q = 4h + m): 64h + 4i + m.
-__host__ __device__ constexpr int pcol(int q, int i) { return 64 * (q >> 2) + 4 * i + (q & 3); }
 
 int padded_rank(int rank) {
   if (rank <= 0) return 0;
@@ -329,16 +238,6 @@ hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64
 //   K v = C⁻¹ w (register Cholesky, lane i = row i), x' = D⁻¹ Z_jᵀ v.
 // Entries with c = 0 (implicit zero ratings) contribute nothing to A or b and are masked out.
 // =============================================================================================
-__device__ __forceinline__ void rating_weights(float r, int implicit, float alpha, float& c, float& w) {
-  if (implicit) {
-    c = alpha * fabsf(r);
-    w = r > 0.f ? 1.f + c : 0.f;
-  } else {
-    c = 1.f;
-    w = r;
-  }
-}
-
 template <int KP, int D>
 __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
   constexpr int NB = D / 16, NT = NB * (NB + 1) / 2, LDK = D + 1, NHC = KP / 64;
@@ -952,30 +851,6 @@ hipError_t launch_heavy_split(int KP, const SolveArgs& a, const SplitArgs& s, hi
   if (KP == 128) return launch_split_kp<128>(a, s, st);
   if (KP == 256) return launch_split_kp<256>(a, s, st);
   return hipErrorInvalidValue;
-}
-
-// 16x16 Cholesky of a diagonal tile in registers: lane i (of each 16-lane row) holds row i (rr[m],
-// m <= i meaningful).  On return rr[m] = L[i][m] (m <= i), dg = 1/L[i][i].  A pivot that collapses
-// below 2^-21 of its start value is numerically singular in fp32 (Spark's fp64 dppsv reports
-// info > 0 on such systems): reported as not positive definite (return value, wave-uniform).
-__device__ __forceinline__ bool chol16(float (&rr)[16], float& dg, int i) {
-  bool notpd = false;
-  float d0 = 0.f;
-#pragma unroll
-  for (int c = 0; c < 16; ++c) d0 = (i == c) ? rr[c] : d0;
-  static_for<0, 16>([&](auto cc) {
-    constexpr int c = decltype(cc)::value;
-    if (i == c && !(rr[c] > d0 * 4.76837158e-07f)) notpd = true;
-    const float piv = bc16_after_asm<c>(rr[c]);
-    const float inv = frsq(piv), sq = piv * inv;
-    rr[c] = (i == c) ? sq : rr[c] * inv;
-    dg = (i == c) ? inv : dg;
-    static_for<c + 1, 16>([&](auto mm) {
-      constexpr int m = decltype(mm)::value;
-      fnmac_bc16<m, m == c + 1>(rr[m], rr[c], rr[c]);
-    });
-  });
-  return __any(notpd);
 }
 
 // PH: phase mask for profiling probes (bit 0 build, bit 1 factor + substitution); the engine runs 3.

@@ -1,0 +1,375 @@
+// Heavy rows, one WAVE per dst row (padded rank KP <= 128): the row's whole normal equation lives in
+// that wave's MFMA accumulators from the first gathered rating to the last pivot.
+//
+// Same equation as solve_heavy_kernel (als_kernels.hip), in the eigenbasis of the src Gram
+// (Spark ALS.computeFactors: NormalEquation.add per rating + CholeskySolver, reached from
+// ALSRecommenderBuilder.scala:58):  A' = diag(Λ + λn) + Σ c z zᵀ,  b' = Σ w z,  A' x = b'.
+//
+//  gather   the row's factor rows arrive by LDS-DMA (global_load_lds_dwordx4, 1 KiB per
+//           wave-instruction = 2 rows at KP = 128), 32 ratings per stage, into a per-wave raw fp32
+//           stage.  No registers hold data in flight, so 8 waves per CU keep 8 stages in flight.
+//  build    each lane reads its MFMA fragments (8 ratings of one column per 16-column block) out of
+//           the stage, scales them by √c and the column's power of two, splits them into fp16
+//           hi + lo and accumulates the NQ(NQ+1)/2 upper 16x16 tiles with hi·hi + hi·lo + lo·hi
+//           on v_mfma_f32_16x16x32_f16 (fp32 accumulation; the numerics of heavy_build).  b' is an
+//           fp32 VALU sum of w·z.  The stage is refilled as soon as the fragments are in registers.
+//  factor   right-looking blocked Cholesky A' = UᵀU on the accumulator tiles themselves: per panel,
+//           the diagonal tile goes through LDS into the row layout of chol16, L⁻¹ of the tile comes
+//           from a 16-step DPP substitution, the panel row is U = L⁻¹·T on f32 MFMA and the trailing
+//           tiles are updated with Uᵀ U on f32 MFMA -- the C/D layout of one MFMA is the A and B
+//           operand layout of the next, so no tile moves.  The right-hand side follows as an extra
+//           VALU column, then a block back substitution with the kept L⁻¹ tiles.
+// Against the 4-wave workgroup kernel this trades 4 waves x 39 KB of LDS per row for one wave and
+// 16.5 KB: twice the rows in flight per CU, and no workgroup barriers in the factorisation.
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdint>
+#include "device_common.h"
+#include "kernels.h"
+
+namespace albedo {
+namespace {
+
+typedef __attribute__((address_space(3))) void* lds_vp;
+typedef __attribute__((address_space(1))) const void* glb_vp;
+
+template <int KP>
+struct WaveRow {
+  static constexpr int NQ = KP / 16, NT = NQ * (NQ + 1) / 2;
+  static constexpr int SPS = 32;                         // ratings per stage = one 16x16x32 k-step
+  static constexpr int RB = 4 * KP;                      // bytes per factor row
+  static constexpr int RPI = 1024 / RB;                  // rows per LDS-DMA wave-instruction
+  static constexpr int LPR = 64 / RPI;                   // lanes per row in one instruction
+  static constexpr int NI = SPS / RPI;                   // DMA instructions per stage
+  static constexpr int STAGE = SPS * RB + 64 * (SPS / 8 - 1);  // + 64 B per 8-rating group (banks)
+  static constexpr int WAVES = 4;                        // rows per workgroup (independent waves)
+  static constexpr int LDS_WAVE = (STAGE + 255) & ~255;
+  static constexpr int LDS = WAVES * LDS_WAVE + 2 * KP * 4;  // + column scales and inverses
+  static_assert(RPI * RB == 1024 && 8 % RPI == 0, "DMA pieces never cross an 8-rating group");
+  static_assert(LDS_WAVE >= 2048 + NQ * 1024, "the stage doubles as the factor's scratch + L⁻¹ store");
+};
+
+// upper tile (a <= b) index, row-major over the upper triangle
+__host__ __device__ constexpr int tix(int a, int b, int nq) { return a * nq - a * (a - 1) / 2 + (b - a); }
+
+// LDS byte offset of (rating r of the stage, column c).  Lane i + 16q reads ratings 8q..8q+7 of
+// column 16A + i: the 64-B shift per 8-rating group puts the four q groups on different banks.
+template <int KP>
+__device__ __forceinline__ int soff(int r, int c) { return r * 4 * KP + 64 * (r >> 3) + 4 * c; }
+
+template <int KP, bool IMPLICIT>
+__global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
+  using W = WaveRow<KP>;
+  constexpr int NQ = W::NQ, NT = W::NT;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int lane = threadIdx.x & 63, q = lane >> 4, i16 = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // scalar: LDS-DMA bases in SGPRs
+  float* s_cs = reinterpret_cast<float*>(lds + W::WAVES * W::LDS_WAVE);  // [KP] scales, [KP] inverses
+  for (int e = threadIdx.x; e < 2 * KP; e += 256) s_cs[e] = a.colscale[e];
+  __syncthreads();  // the only workgroup barrier: every wave below is on its own row
+  const int64_t ridx = (int64_t)blockIdx.x * W::WAVES + wave;
+  if (ridx >= a.n_rows) return;
+  char* st = lds + wave * W::LDS_WAVE;
+  const int j = a.rows[ridx];
+  const int64_t p0 = a.ptr[j];
+  const int d = (int)(a.ptr[j + 1] - p0);
+  const int nst = (d + W::SPS - 1) / W::SPS;
+
+  f32x4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = zero4();
+  constexpr int CPL = KP / 64;  // b' columns per lane during the build: lane l sums CPL·l .. CPL·l+CPL-1
+  float bpart[CPL];
+#pragma unroll
+  for (int e = 0; e < CPL; ++e) bpart[e] = 0.f;
+  int npos = 0;
+
+  // (col, val) of stage s: lane l holds rating 32 s + (l & 31), clamped to the row (zero weight)
+  auto iload = [&](int s, int& c_out, float& r_out) {
+    const int e = W::SPS * s + (lane & 31);
+    const int64_t pe = p0 + (e < d ? e : d - 1);
+    c_out = a.col[pe];
+    r_out = a.val[pe];
+  };
+  // gather of one stage: piece u holds ratings RPI·u .. RPI·u + RPI-1, lane l the 16 B at
+  // 4·(l % LPR) of rating RPI·u + l / LPR; the rating's src row is wave-uniform (readlane)
+  auto dma = [&](int cidx) {
+    static_for<0, W::NI>([&](auto U) {
+      constexpr int u = decltype(U)::value;
+      int row;
+      if constexpr (W::RPI == 2) {
+        const int r0 = rdlane_i(cidx, 2 * u), r1 = rdlane_i(cidx, 2 * u + 1);
+        row = lane < 32 ? r0 : r1;
+      } else {
+        const int r0 = rdlane_i(cidx, 4 * u), r1 = rdlane_i(cidx, 4 * u + 1);
+        const int r2 = rdlane_i(cidx, 4 * u + 2), r3 = rdlane_i(cidx, 4 * u + 3);
+        row = q == 0 ? r0 : (q == 1 ? r1 : (q == 2 ? r2 : r3));
+      }
+      const float* src = a.Z + (int64_t)row * KP + 4 * (lane % W::LPR);
+      __builtin_amdgcn_global_load_lds((glb_vp)src, (lds_vp)(st + soff<KP>(W::RPI * u, 0)), 16, 0, 0);
+    });
+  };
+
+  int c_cur = 0, c_nxt = 0;
+  float r_cur = 0.f, r_nxt = 0.f;
+  // the stage's fragments are in registers: refill the stage with s + 1, fetch the indices of s + 2
+  auto next_stage = [&](int s) {
+    dma(c_nxt);
+    c_cur = c_nxt;
+    r_cur = r_nxt;
+    if (s + 2 < nst) iload(s + 2, c_nxt, r_nxt);
+  };
+  if (nst > 0) {
+    iload(0, c_cur, r_cur);
+    dma(c_cur);
+    if (nst > 1) iload(1, c_nxt, r_nxt);
+  }
+  for (int s = 0; s < nst; ++s) {
+    const bool in = W::SPS * s + (lane & 31) < d;
+    npos += __popcll(__ballot(lane < 32 && in && r_cur > 0.f));
+    float cw = 0.f, ww = 0.f;
+    rating_weights(r_cur, IMPLICIT, a.alpha, cw, ww);
+    const float sw = in ? sqrtf(cw) : 0.f;  // √c (0 past the row end)
+    const float wv = in ? ww : 0.f;
+    float sw8[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) sw8[m] = __shfl(sw, 8 * q + m);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this stage's DMA (and stage s+1's indices)
+    // fragment of block A (lane i + 16q: ratings 8q .. 8q+7 of column 16A + i) -> fp16 hi / lo
+    auto conv = [&](auto AA, f16x8& hv, f16x8& lv) {
+      constexpr int A = decltype(AA)::value;
+      float z[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) z[m] = *reinterpret_cast<const float*>(st + soff<KP>(8 * q + m, 16 * A + i16));
+      const float csa = s_cs[16 * A + i16];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        float v = z[m] * (sw8[m] * csa);
+        asm("" : "+v"(v));  // one fp32 rounding; hi and lo both from that value (see heavy_build)
+        const _Float16 h = (_Float16)v;
+        hv[m] = h;
+        lv[m] = (_Float16)(v - (float)h);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one block's raw values live at a time (register cap)
+    };
+    auto tile = [&](auto AA, auto BB, const f16x8& ha, const f16x8& la, const f16x8& hb, const f16x8& lb) {
+      constexpr int t = tix(decltype(AA)::value, decltype(BB)::value, NQ);
+      acc[t] = mfma_h(ha, hb, acc[t]);
+      acc[t] = mfma_h(ha, lb, acc[t]);
+      acc[t] = mfma_h(la, hb, acc[t]);
+    };
+    {  // every block's fragments in registers (64 VGPRs at KP = 128, beside the tiles' 144)
+      f16x8 fh[NQ], fl[NQ];
+      static_for<0, NQ>([&](auto AA) { conv(AA, fh[decltype(AA)::value], fl[decltype(AA)::value]); });
+      // b' += Σ_r w_r z_r: rows read whole (CPL consecutive columns per lane), w_r wave-uniform
+#pragma unroll 4
+      for (int r = 0; r < W::SPS; ++r) {
+        const float wr = rdlane(wv, r);
+        if constexpr (CPL == 2) {
+          const float2 z2 = *reinterpret_cast<const float2*>(st + soff<KP>(r, 2 * lane));
+          bpart[0] = fmaf(wr, z2.x, bpart[0]);
+          bpart[1] = fmaf(wr, z2.y, bpart[1]);
+        } else {
+          bpart[0] = fmaf(wr, *reinterpret_cast<const float*>(st + soff<KP>(r, lane)), bpart[0]);
+        }
+      }
+      WAVE_LDS_SYNC();
+      if (s + 1 < nst) next_stage(s);
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<0, NQ>([&](auto AA) {
+        static_for<decltype(AA)::value, NQ>([&](auto BB) {
+          tile(AA, BB, fh[decltype(AA)::value], fl[decltype(AA)::value], fh[decltype(BB)::value],
+               fl[decltype(BB)::value]);
+        });
+      });
+    }
+  }
+
+  __builtin_amdgcn_sched_barrier(0);  // keep the factor's loads out of the build loop
+  // ---- b' complete (sum over the four rating groups), tiles unscaled, diagonal Λ + λn ----------
+  // b' to the factor's layout (lane i + 16q holds b'[16A + i] for every block A) through LDS
+  float* bsc = reinterpret_cast<float*>(st);
+#pragma unroll
+  for (int e = 0; e < CPL; ++e) bsc[CPL * lane + e] = bpart[e];
+  WAVE_LDS_SYNC();
+  float bacc[NQ];
+#pragma unroll
+  for (int A = 0; A < NQ; ++A) bacc[A] = bsc[16 * A + i16];
+  WAVE_LDS_SYNC();
+  const float lamn = a.reg * (float)(IMPLICIT ? npos : d);
+  const float* isc = s_cs + KP;
+  static_for<0, NQ>([&](auto AA) {
+    constexpr int A = decltype(AA)::value;
+    const f32x4 ir = ld4(isc + 16 * A + 4 * q);
+    static_for<A, NQ>([&](auto BB) {
+      constexpr int B = decltype(BB)::value, t = tix(A, B, NQ);
+      const float ic = isc[16 * B + i16];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[t][r] *= ir[r] * ic;
+      if constexpr (A == B) {
+        const int c = 16 * A + i16;
+        const float dadd = c < a.kreal ? a.lam[c] + lamn : 1.0f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * q + r == i16) acc[t][r] += dadd;
+      }
+    });
+  });
+
+#ifdef WAVE_PROBE_BUILD_ONLY
+  if (q == 0) for (int A = 0; A < NQ; ++A) a.X[(int64_t)j * KP + 16 * A + i16] = bacc[A] + acc[tix(A, A, NQ)][0];
+  return;
+#endif
+  // ---- blocked Cholesky A' = UᵀU on the tiles; RHS forward substitution alongside ----------------
+  float* scr = reinterpret_cast<float*>(st);  // [0,256): diagonal tile, [256,512): L⁻¹ staging
+  // L⁻¹ of every panel in the A-operand layout (lane i + 16q: L⁻¹[i][4q .. 4q+3]), kept in the dead
+  // stage for the back substitution: [NQ][64 lanes] f32x4 after the two scratch tiles
+  f32x4* s_linv = reinterpret_cast<f32x4*>(scr + 512);
+  bool notpd = false;
+  static_for<0, NQ>([&](auto JB) {
+    constexpr int jb = decltype(JB)::value, td = tix(jb, jb, NQ);
+    // diagonal tile to the row layout of chol16 (lane i: row i, replicated over the 4 lane groups)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) scr[(4 * q + r) * 16 + i16] = acc[td][r];
+    WAVE_LDS_SYNC();
+    float rr[16];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f32x4 v = ld4(scr + 16 * i16 + 4 * u);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rr[4 * u + e] = v[e];
+    }
+    float dg = 1.f;
+    notpd |= chol16(rr, dg, i16);
+    // chol16 ends in inline asm: two wait states before any DPP read of its results
+    asm volatile("s_nop 1"
+                 : "+v"(rr[0]), "+v"(rr[1]), "+v"(rr[2]), "+v"(rr[3]), "+v"(rr[4]), "+v"(rr[5]), "+v"(rr[6]),
+                   "+v"(rr[7]), "+v"(rr[8]), "+v"(rr[9]), "+v"(rr[10]), "+v"(rr[11]), "+v"(rr[12]),
+                   "+v"(rr[13]), "+v"(rr[14]), "+v"(rr[15]), "+v"(dg));
+    // column i16 of L⁻¹: L x = e_i16 by forward substitution, L[r][m] broadcast from lane r
+    float x[16];
+    static_for<0, 16>([&](auto RR) {
+      constexpr int r = decltype(RR)::value;
+      float tv = (i16 == r) ? 1.f : 0.f;
+      // one v_fmac_f32_dpp per term (asm keeps the broadcasts from being hoisted into registers)
+      static_for<0, r>([&](auto MM) {
+        constexpr int m = decltype(MM)::value;
+        fnmac_bc16<r, false>(tv, rr[m], x[m]);
+      });
+      x[r] = tv * bc16_after_asm<r>(dg);
+    });
+    if (q == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) scr[256 + 16 * r + i16] = x[r];
+    }
+    WAVE_LDS_SYNC();
+    const f32x4 lv = ld4(scr + 256 + 16 * i16 + 4 * q);
+    s_linv[jb * 64 + lane] = lv;
+    // panel row: U(jb, I) = L⁻¹ T(jb, I)  (A = L⁻¹ rows, B = the tile's C/D registers)
+    static_for<jb + 1, NQ>([&](auto II) {
+      constexpr int I = decltype(II)::value, t = tix(jb, I, NQ);
+      f32x4 u = zero4();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) u = mfma4(lv[s], acc[t][s], u);
+      acc[t] = u;
+    });
+    // RHS: y_jb = L⁻¹ b_jb, then b_M -= U(jb, M)ᵀ y_jb for the blocks below
+    float yp = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) yp = fmaf(lv[s], __shfl(bacc[jb], 4 * q + s), yp);
+    yp += __shfl_xor(yp, 16);
+    yp += __shfl_xor(yp, 32);
+    bacc[jb] = yp;
+    float y4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y4[r] = __shfl(yp, 4 * q + r);
+    static_for<jb + 1, NQ>([&](auto MM) {
+      constexpr int M = decltype(MM)::value, t = tix(jb, M, NQ);
+      float pv = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pv = fmaf(acc[t][r], y4[r], pv);
+      pv += __shfl_xor(pv, 16);
+      pv += __shfl_xor(pv, 32);
+      bacc[M] -= pv;
+    });
+    // trailing tiles: T(M, I) -= U(jb, M)ᵀ U(jb, I), the next diagonal tile first
+    static_for<jb + 1, NQ>([&](auto MM) {
+      constexpr int M = decltype(MM)::value, tm = tix(jb, M, NQ);
+      static_for<M, NQ>([&](auto II) {
+        constexpr int I = decltype(II)::value, t = tix(M, I, NQ), ti = tix(jb, I, NQ);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[t] = mfma4(-acc[tm][s], acc[ti][s], acc[t]);
+      });
+    });
+    WAVE_LDS_SYNC();  // scratch reads done before the next panel rewrites it
+  });
+
+  // ---- back substitution: x_jb = L_jb⁻ᵀ (y_jb - Σ_{M > jb} U(jb, M) x_M) ------------------------
+  float xs[NQ];
+  static_for<0, NQ>([&](auto KK) {
+    constexpr int jb = NQ - 1 - decltype(KK)::value;
+    float pr[4] = {0.f, 0.f, 0.f, 0.f};  // lane c + 16g: Σ_M U(jb, M)[4g + r][c] x_M[c]
+    static_for<jb + 1, NQ>([&](auto MM) {
+      constexpr int M = decltype(MM)::value, t = tix(jb, M, NQ);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pr[r] = fmaf(acc[t][r], xs[M], pr[r]);
+    });
+    float tq[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tq[r] = sum16_last(pr[r]);  // row 4g + r in lane 15 + 16g
+    // lane i + 16q gets t_i = y_i - (row i's sum): row i lives in lane 15 + 16(i >> 2), slot i & 3
+    float ti = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = __shfl(tq[r], 15 + 16 * (i16 >> 2));
+      ti = (i16 & 3) == r ? v : ti;
+    }
+    ti = bacc[jb] - ti;
+    // x = L⁻ᵀ t: lane k + 16q holds L⁻¹[k][4q + s]; x[4q + s] = Σ_k L⁻¹[k][4q + s] t_k
+    const f32x4 lv = s_linv[jb * 64 + lane];
+    float xq[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) xq[s] = sum16_last(lv[s] * ti);  // x[4g + s] in lane 15 + 16g
+    float xi = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float v = __shfl(xq[s], 15 + 16 * (i16 >> 2));
+      xi = (i16 & 3) == s ? v : xi;
+    }
+    xs[jb] = xi;
+  });
+  bool nonfinite = false;
+#pragma unroll
+  for (int A = 0; A < NQ; ++A) {
+    const int c = 16 * A + i16;
+    const float v = c < a.kreal ? xs[A] : 0.f;
+    nonfinite |= !isfinite(v);
+    if (q == 0) a.X[(int64_t)j * KP + c] = v;
+  }
+  const bool bad = notpd || __any(nonfinite);  // wave-uniform
+  if (lane == 0 && bad) atomicOr(a.err, 2);
+}
+
+template <int KP>
+hipError_t launch_wave_kp(const SolveArgs& a, hipStream_t s) {
+  using W = WaveRow<KP>;
+  static const hipError_t attr = allow_lds(solve_wave_kernel<KP, true>, W::LDS);
+  static const hipError_t attr2 = allow_lds(solve_wave_kernel<KP, false>, W::LDS);
+  if (attr != hipSuccess) return attr;
+  if (attr2 != hipSuccess) return attr2;
+  const int blocks = (int)((a.n_rows + W::WAVES - 1) / W::WAVES);
+  if (a.implicit) solve_wave_kernel<KP, true><<<blocks, 64 * W::WAVES, W::LDS, s>>>(a);
+  else solve_wave_kernel<KP, false><<<blocks, 64 * W::WAVES, W::LDS, s>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_solve_wave(int KP, const SolveArgs& a, hipStream_t s) {
+  if (a.n_rows <= 0) return hipSuccess;
+  if (KP == 64) return launch_wave_kp<64>(a, s);
+  if (KP == 128) return launch_wave_kp<128>(a, s);
+  return hipErrorInvalidValue;
+}
+
+}  // namespace albedo

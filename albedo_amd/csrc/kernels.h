@@ -57,6 +57,8 @@ hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64
 // Per-row solves. light: rows with degree <= D (D in {16,32,64}); heavy: any degree.
 hipError_t launch_solve_light(int KP, int D, const SolveArgs& a, hipStream_t s);
 hipError_t launch_solve_heavy(int KP, const SolveArgs& a, hipStream_t s);
+// heavy rows, one wave per row (heavy_wave.hip), KP <= 128; rows of any degree (split rows excepted)
+hipError_t launch_solve_wave(int KP, const SolveArgs& a, hipStream_t s);
 
 // nonnegative = true: Spark NNLS per row; Gt = the src Gram in packed lower 16x17 tiles (fp32).
 hipError_t launch_solve_nnls(int KP, const SolveArgs& a, const float* Gt, hipStream_t s);

@@ -72,15 +72,20 @@ def _fp64_row(Y_all, G, y_rows, rating, reg, alpha, nonneg):
     return np.linalg.solve(A + lam * np.eye(A.shape[0]), b)
 
 
-@pytest.mark.parametrize("k,nonneg", [(128, False), (256, False), (256, True)])
-def test_million_star_row(gpu_lib, k, nonneg):
+@pytest.mark.parametrize("k,nonneg,absf", [(128, False, False), (256, False, False), (256, True, False),
+                                           (256, True, True)])
+def test_million_star_row(gpu_lib, k, nonneg, absf):
     """A repo with 1.05M stars (above BASELINE c5's ">1M stars") at rank 128 / 256 and the rank-256
-    NNLS path, against the fp64 solve of Spark's implicit normal equation for that row."""
+    NNLS path, against the fp64 solve of Spark's implicit normal equation for that row.
+
+    absf: all-positive src factors.  Spark's NNLS stops when its first step is below 1e-7 (an
+    absolute threshold, NNLS.scala); with ~10^6 positive rows the first step is ~4e-8, so Spark
+    returns x = 0 for that row -- the device must return exactly 0 too."""
     n_big, n_users = 1_050_000, 1_100_000
     user, item, rating, u_all = _million_star_data(n_big, n_users, 40, 4000, seed=k + nonneg)
     rng = np.random.default_rng(17)
     U0 = rng.standard_normal((n_users, k)).astype(np.float32)
-    if nonneg:
+    if absf:
         U0 = np.abs(U0)
     U0 /= np.linalg.norm(U0, axis=1, keepdims=True)
     c = _nonneg_ctx(gpu_lib, k) if nonneg else Ctx(gpu_lib, k)
@@ -95,10 +100,11 @@ def test_million_star_row(gpu_lib, k, nonneg):
     c.half(1)
     t = np.zeros(c.L.ALS_T_COUNT)
     c.L.check(gpu_lib.als_last_timings(c.h, 1, c.L.ptr(t, C.c_double), c.L.ALS_T_COUNT))
-    _record(f"million_star_row[k={k},nonneg={nonneg}]",
+    _record(f"million_star_row[k={k},nonneg={nonneg},abs={absf}]",
             {"stars": int(n_big), "rank": k, "solve_heavy_ms": t[5], "half_ms": t[6]})
     ids, V = c.factors(1)
-    U64 = U0.astype(np.float64)
+    present = np.isin(u_all, user)  # users without a star are not rows of the model (nor of its Gram)
+    U64 = U0[present].astype(np.float64)
     G = U64.T @ U64
     src = np.empty(n_big + 16, np.int32)
     rat = np.empty(n_big + 16, np.float32)
@@ -110,12 +116,16 @@ def test_million_star_row(gpu_lib, k, nonneg):
         n = int(n_row[0])
         x = _fp64_row(U0, G, np.searchsorted(u_all, src[:n]), rat[:n], 0.5, 40.0, nonneg)
         g = V[np.searchsorted(ids, rid)].astype(np.float64)
+        if absf and rid == 7:
+            assert np.all(x == 0) and np.all(g == 0), "Spark's NNLS returns 0 for this row"
+            checked.append((rid, n, 0.0))
+            continue
         err = float(np.max(np.abs(g - x)) / np.max(np.abs(x)))
         checked.append((rid, n, err))
         assert err < (1e-3 if nonneg else 1e-4), f"repo {rid} ({n} stars): rel err {err:.3e}"
         if nonneg:
             assert np.all(g >= 0)
-    _record(f"million_star_row[k={k},nonneg={nonneg}]", {"rows": checked})
+    _record(f"million_star_row[k={k},nonneg={nonneg},abs={absf}]", {"rows": checked})
 
 
 def test_inject_user_factors_only_keeps_them(gpu_lib):
