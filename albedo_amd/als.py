@@ -16,8 +16,6 @@ All compute runs on the MI355X through the C ABI; there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
-import json
-import os
 import time
 
 import numpy as np
@@ -79,7 +77,11 @@ class _Params:
                 device="HIP device ordinal (-1 = current)",
                 lightMaxDegree="rows with <= this many ratings use the push-through solve (-1 default, 0 off)")
 
-    def __init__(self, **kw):
+    _uid_prefix = "als"
+
+    def __init__(self, uid=None, **kw):
+        from .persistence import random_uid
+        self.uid = uid or random_uid(self._uid_prefix)  # Identifiable.randomUID("als")
         self._p = dict(self._defaults)
         for k, v in kw.items():
             self._set(k, v)
@@ -148,7 +150,7 @@ class ALS(_Params):
 
     def _param_map(self, pm):
         """Validate a ParamMap (dict of param name -> value) like Params.copy(extra)."""
-        probe = ALS(**self._p)
+        probe = ALS(uid=self.uid, **self._p)
         for k, v in pm.items():
             probe._set(k, v)
         return dict(probe._p)
@@ -191,7 +193,7 @@ class ALS(_Params):
         except Exception:
             lib.als_destroy(h)
             raise
-        model = ALSModel(h, pm)
+        model = ALSModel(h, pm, uid=self.uid)
         model.fit_seconds = fit_s
         return model
 
@@ -230,7 +232,7 @@ class ALS(_Params):
                 check(lib.als_model_create(k, ui.size, ptr(ui, C.c_int32), ptr(uf, C.c_float), ii.size,
                                            ptr(ii, C.c_int32), ptr(itf, C.c_float), int(pm["device"]),
                                            C.byref(mh)))
-                m = ALSModel(mh, pm)
+                m = ALSModel(mh, pm, uid=self.uid)
                 m._cache.update(f)
                 m.fit_seconds = fit_s
                 models.append(m)
@@ -243,8 +245,8 @@ class ALS(_Params):
 class ALSModel(_Params):
     """Spark ml.recommendation.ALSModel over an engine context holding both factor matrices."""
 
-    def __init__(self, handle, params):
-        super().__init__()
+    def __init__(self, handle, params, uid=None):
+        super().__init__(uid=uid)
         self._p.update(params)
         self._h = handle
         self._cache = {}
@@ -352,29 +354,13 @@ class ALSModel(_Params):
         return self._rec_frame(*self._recommend(_lib.ALS_ITEM, numUsers, items), self._p["itemCol"],
                                self._p["userCol"])
 
-    # ---- persistence (Spark ML layout: metadata/part-00000 + userFactors/ + itemFactors/ parquet) ---
-    def save(self, path, overwrite=False):
-        import shutil
-        import pyarrow as pa
-        import pyarrow.parquet as pq
-        if os.path.exists(path):
-            if not overwrite:
-                raise IOError(f"Path {path} already exists. To overwrite it, please use write.overwrite().save(path).")
-            shutil.rmtree(path)
-        os.makedirs(os.path.join(path, "metadata"))
-        meta = {"class": "org.apache.spark.ml.recommendation.ALSModel", "timestamp": int(time.time() * 1000),
-                "sparkVersion": "2.2.0", "uid": "als_albedo_mi355x",
-                "paramMap": {k: self._p[k] for k in ("userCol", "itemCol", "predictionCol", "coldStartStrategy")},
-                "rank": self.rank}
-        with open(os.path.join(path, "metadata", "part-00000"), "w") as fh:
-            fh.write(json.dumps(meta, separators=(",", ":")) + "\n")
-        open(os.path.join(path, "metadata", "_SUCCESS"), "w").close()
-        for name, (ids, f) in (("userFactors", self.user_factors_np()), ("itemFactors", self.item_factors_np())):
-            os.makedirs(os.path.join(path, name))
-            table = pa.table({"id": pa.array(ids, pa.int32()),
-                              "features": pa.array(list(f), pa.list_(pa.float32()))})
-            pq.write_table(table, os.path.join(path, name, "part-00000.parquet"))
-            open(os.path.join(path, name, "_SUCCESS"), "w").close()
+    # ---- persistence (Spark 2.2 ALSModelWriter / ALSModelReader layout: albedo_amd/persistence.py) ----
+    MODEL_PARAMS = ("userCol", "itemCol", "predictionCol", "coldStartStrategy")  # ALSModelParams
+
+    def save(self, path, overwrite=False, rows_per_part=1 << 20):
+        from . import persistence
+        persistence.save_als_model(path, self.uid, {k: self._p[k] for k in self.MODEL_PARAMS}, self.rank,
+                                   self.user_factors_np(), self.item_factors_np(), overwrite, rows_per_part)
 
     def write(self):
         model = self
@@ -393,29 +379,14 @@ class ALSModel(_Params):
 
     @classmethod
     def load(cls, path, device=-1):
-        import glob
-        import pyarrow.parquet as pq
-        with open(os.path.join(path, "metadata", "part-00000")) as fh:
-            meta = json.loads(fh.readline())
+        from . import persistence
+        meta, (uid, uf), (iid, itf) = persistence.load_als_model(path)
         rank = int(meta["rank"])
-
-        def read(name):
-            parts = sorted(glob.glob(os.path.join(path, name, "*.parquet")))
-            ids, feats = [], []
-            for p in parts:
-                t = pq.read_table(p)
-                ids.append(np.asarray(t.column("id").to_numpy(), dtype=np.int32))
-                feats.append(np.asarray(t.column("features").to_pylist(), dtype=np.float32).reshape(-1, rank))
-            if not parts:
-                return np.empty(0, np.int32), np.empty((0, rank), np.float32)
-            return np.concatenate(ids), np.concatenate(feats)
-
-        uid, uf = read("userFactors")
-        iid, itf = read("itemFactors")
         h = C.c_void_p()
         check(load().als_model_create(rank, uid.size, ptr(uid, C.c_int32), ptr(uf, C.c_float), iid.size,
                                       ptr(iid, C.c_int32), ptr(itf, C.c_float), int(device), C.byref(h)))
         params = dict(_Params._defaults)
-        params.update(meta.get("paramMap", {}))
+        params.update({k: v for k, v in meta.get("paramMap", {}).items() if k in _Params._defaults})
         params["rank"] = rank
-        return cls(h, params)
+        model = cls(h, params, uid=meta.get("uid"))
+        return model

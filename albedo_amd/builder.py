@@ -13,8 +13,10 @@ Same protocol as the reference job:
      loadUserActualItemsDF(30) = intoUserActualItems(starred_at desc)          (:92-104)
 
 Differences, all forced by the environment: the MySQL dump (README.md:29) is not available
-offline, so step 1 uses the seeded synthetic GitHub-like star matrix (albedo_amd.synthetic,
-SURVEY.md §8(d)) with per-star timestamps; the reference's split and sample are unseeded
+offline, so step 1's loadOrCreateDataFrame creates the parquet cache from the seeded synthetic
+GitHub-like star matrix (albedo_amd.synthetic) with per-star timestamps instead
+of the JDBC read (an existing rawStarringDF.parquet -- e.g. one exported from the real dump -- is
+read as is); the reference's split and sample are unseeded
 (`randomSplit` without a seed, `scala.util.Random.shuffle`), here they take `--seed`; the fixed
 user 652070 is used when present, else the highest user id of the test split.
 """
@@ -26,7 +28,7 @@ import time
 
 import numpy as np
 
-from . import settings
+from . import persistence, settings
 from .als import ALS, ALSModel
 from .evaluation import RankingEvaluator, into_user_items
 from .recommenders import ALSRecommender
@@ -45,12 +47,23 @@ def load_or_create_model(model_cls, path, create_model_func):
     return model_cls.load(path)
 
 
-def load_raw_starring(users=20000, repos=4000, stars=400000, seed=42):
-    """Stand-in for DatasetUtils.loadRawStarringDS (:111-123): dict of columns user_id, repo_id,
-    starred_at (epoch seconds), starring (= 1.0, :118)."""
+def synthetic_starring(users=20000, repos=4000, stars=400000, seed=42):
+    """Stand-in for the JDBC read of app_repostarring (DatasetUtils.scala:116-118): dict of columns
+    user_id, repo_id, starred_at (datetime64[s]), starring (= 1.0, :118)."""
     d = generate(SynthSpec(users, repos, stars, seed=seed), with_timestamps=True)
-    return {"user_id": d["user"], "repo_id": d["item"], "starred_at": d["ts"],
+    return {"user_id": d["user"], "repo_id": d["item"], "starred_at": d["ts"].astype("datetime64[s]"),
             "starring": d["rating"].astype(np.float64)}
+
+
+def load_raw_starring(users=20000, repos=4000, stars=400000, seed=42, path=None):
+    """DatasetUtils.loadRawStarringDS (:111-123): loadOrCreateDataFrame(dataDir/today/
+    rawStarringDF.parquet, <read app_repostarring + starring = 1.0>) -- the parquet cache is read
+    when present, else the synthetic stand-in is written there first.  `path=False` skips the
+    cache (pure in-memory)."""
+    if path is False:
+        return synthetic_starring(users, repos, stars, seed)
+    return persistence.load_or_create_dataframe(path or settings.raw_starring_path(),
+                                                lambda: synthetic_starring(users, repos, stars, seed))
 
 
 def sample_test_users(stars, seed, n=250):
@@ -74,9 +87,11 @@ def main(argv=None):
     ap.add_argument("--top-k", type=int, default=30)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--model-path", default=None)
+    ap.add_argument("--starring-path", default=None,
+                    help="parquet directory of Starring rows (default dataDir/today/rawStarringDF.parquet)")
     args = ap.parse_args(argv)
 
-    stars = load_raw_starring(args.users, args.repos, args.stars, args.seed)
+    stars = load_raw_starring(args.users, args.repos, args.stars, args.seed, path=args.starring_path)
     path = args.model_path or settings.als_model_path()
 
     def fit():

@@ -102,6 +102,7 @@ struct Side {
   bool has_factors = false;
   double t[ALS_T_COUNT] = {0};
   int64_t stats[4] = {0};
+  int64_t solver[4] = {0};       // NNLS iterations: sum over rows, max, rows (last half-sweep)
   DevBuf d_orig;                 // [n][KP] original-basis factors, dense order (materialised)
   bool orig_valid = false;
   // split-K of the heavy tail: the first n_split heavy rows (degree > split chunk), their chunks
@@ -128,6 +129,7 @@ struct als_ctx {
   bool model_only = false;
   DevBuf slab, d_G, d_P, d_lam, d_err, d_Gt, d_cs, d_csmax;
   DevBuf d_partial, d_reduced;   // split-K partial / reduced A' records (shared by both sides)
+  DevBuf d_iters;                // NNLS iteration counters (sum, max)
   int split_len = 0;             // ratings per split-K chunk (0: no split)
   std::vector<float> h_P32, h_lam32, h_Gt;  // host staging of async H2D copies (outlive the sync)
   int slab_blocks = 0;
@@ -206,27 +208,21 @@ int allgather_rows(als_ctx* c, float* buf, int64_t rows_per_rank) {
   return ALS_OK;
 }
 
-// padded position of dense row i of side S
-inline int64_t padded_pos(const Side& S, int64_t i) {
-  const auto it = std::upper_bound(S.starts.begin(), S.starts.end(), i);
-  const int64_t r = (int64_t)(it - S.starts.begin()) - 1;
-  return r * S.maxrows + (i - S.starts[r]);
-}
-
-// Ratings per split-K chunk.  A heavy row accumulates its A' in fp32 MFMA accumulators; beyond a
-// few hundred MFMA steps the accumulation error grows past the 1e-4 row tolerance (a 1.05M-star
-// row measured 4e-4) and one workgroup gathering a 10^6-star row is the launch's tail (45.9 ms for
-// 1.05M stars at rank 128).  8192 ratings = 256 MFMA steps per partial, summed in fp64.
-// ALBEDO_SPLIT_CHUNK overrides it for tuning (0 disables the split).
-// Heavy rows at padded rank <= 128 run one wave per row (heavy_wave.hip) unless ALBEDO_HEAVY=wg
-// selects the 4-wave workgroup kernel (A/B measurements); rank 256 always uses the workgroup kernel.
-bool use_wave_kernel(const als_ctx* c);
-
+// Ratings per split-K chunk.  One workgroup gathering a 10^6-star row is the launch's tail (45.9
+// ms for 1.05M stars at rank 128, more than a whole c4 half-sweep at 8 GPUs), and a partial of 8192
+// ratings keeps every fp32 MFMA accumulation to 256 steps before the fp64 sum (a 1.05M-star row then
+// matches the fp64 solve to 7e-7, tests/test_gpu_heavy_tail.py).  ALBEDO_SPLIT_CHUNK overrides it
+// for tuning (0 disables the split): 2048 / 4096 / 16384 measured 338 / 324 / 311 ms per c4 sweep
+// against 316 ms.
 int split_chunk_len() {
   const char* e = std::getenv("ALBEDO_SPLIT_CHUNK");
   if (e && *e) return std::max(0, std::atoi(e));
   return 8192;
 }
+
+// Heavy rows at padded rank <= 128 run one wave per row (heavy_wave.hip) unless ALBEDO_HEAVY=wg
+// selects the 4-wave workgroup kernel (A/B measurements); rank 256 always uses the workgroup kernel.
+bool use_wave_kernel(const als_ctx* c);
 
 // Everything that depends on the rank / light-row limit rather than on the ratings: degree buckets
 // (the light limit follows KP), factor and rotated-factor buffers, Gram slabs.  Called after ingest
@@ -373,11 +369,12 @@ int ingest_device(als_ctx* c, int64_t n, const int32_t* d_user, const int32_t* d
     HIPCHK(hipMemcpy(S.d_val.p, F.val.as<float>() + e0, S.own_nnz * 4, hipMemcpyDeviceToDevice));
     if (c->world == 1) {
       HIPCHK(hipMemcpy(S.d_col.p, F.col.as<int32_t>() + e0, S.own_nnz * 4, hipMemcpyDeviceToDevice));
-    } else {  // dense src index -> padded src position
-      std::vector<int32_t> hc(S.own_nnz);
-      HIPCHK(hipMemcpy(hc.data(), F.col.as<int32_t>() + e0, S.own_nnz * 4, hipMemcpyDeviceToHost));
-      for (auto& v : hc) v = (int32_t)padded_pos(Src, v);
-      HIPCHK(hipMemcpy(S.d_col.p, hc.data(), S.own_nnz * 4, hipMemcpyHostToDevice));
+    } else {  // dense src index -> padded src position, on the device
+      ShardStarts ss{};
+      ss.world = c->world;
+      for (int r = 0; r <= c->world; ++r) ss.s[r] = Src.starts[r];
+      HIPCHK(padded_remap(F.col.as<int32_t>() + e0, S.own_nnz, ss, Src.maxrows, S.d_col.as<int32_t>(), st));
+      HIPCHK(hipStreamSynchronize(st));
     }
     S.h_deg.resize(S.own_n);
     for (int64_t r = 0; r < S.own_n; ++r) S.h_deg[r] = lp[r + 1] - lp[r];
@@ -491,6 +488,9 @@ int half_sweep_nnls(als_ctx* c, int t) {
   a.reg = (float)c->p.reg_param;
   a.err = c->d_err.as<int>();
   a.colscale = c->d_cs.as<float>();
+  HIPCHK(c->d_iters.ensure(16));
+  HIPCHK(hipMemsetAsync(c->d_iters.p, 0, 16, st));
+  a.iters = c->d_iters.as<unsigned long long>();
   TRYC(heavy_launches(c, T, a, 0, T.boff[B_HEAVY], true));
   TRYC(heavy_launches(c, T, a, T.boff[B_HEAVY], T.boff[NBUCKET] - T.boff[B_HEAVY], true));
   a.n_rows = T.boff[NBUCKET];
@@ -499,8 +499,13 @@ int half_sweep_nnls(als_ctx* c, int t) {
   T.stats[3] = T.own_nnz;
   HIPCHK(hipEventRecord(ev[6], st));
   int err = 0;
+  unsigned long long it[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(&err, c->d_err.p, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(it, c->d_iters.p, 16, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  T.solver[0] = (int64_t)it[0];
+  T.solver[1] = (int64_t)it[1];
+  T.solver[2] = T.boff[NBUCKET];
   T.t[ALS_T_GRAM] = event_ms(ev[0], ev[1]);
   T.t[ALS_T_EIG] = 0.0;
   T.t[ALS_T_ROTATE] = event_ms(ev[2], ev[3]);
@@ -826,6 +831,7 @@ int als_comm_unique_id(void* out128) {
 
 int als_comm_init(als_ctx* c, int32_t rank, int32_t world, const void* id128) {
   if (!c || !id128 || world < 1 || rank < 0 || rank >= world) return fail(ALS_E_INVALID_ARGUMENT, "bad comm args");
+  if (world > 16) return fail(ALS_E_UNSUPPORTED, "at most 16 ranks (one node)");
   if (c->has_ratings) return fail(ALS_E_STATE, "als_comm_init must precede als_set_ratings");
   TRYC(set_device(c));
   c->rank = rank;
@@ -842,6 +848,7 @@ int als_comm_init_host(als_ctx* c, int32_t rank, int32_t world, int (*allreduce)
                        int (*allgather)(void*, float*, int64_t), void* user) {
   if (!c || world < 1 || rank < 0 || rank >= world || !allreduce || !allgather)
     return fail(ALS_E_INVALID_ARGUMENT, "bad comm args");
+  if (world > 16) return fail(ALS_E_UNSUPPORTED, "at most 16 ranks (one node)");
   if (c->has_ratings) return fail(ALS_E_STATE, "als_comm_init_host must precede als_set_ratings");
   c->rank = rank;
   c->world = world;
@@ -1046,7 +1053,9 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   if (!c || (side != 0 && side != 1) || !dst_ids_out || !scores_out)
     return fail(ALS_E_INVALID_ARGUMENT, "bad args");
   if (k <= 0) return fail(ALS_E_INVALID_ARGUMENT, "num must be positive");
-  if (k > TOPK_KC) return fail(ALS_E_UNSUPPORTED, "top-k above 64 is not supported by this engine version");
+  if (k > TOPK_MAX)
+    return fail(ALS_E_UNSUPPORTED, "num above " + std::to_string(TOPK_MAX) + " is not supported by this engine");
+  const bool exact_only = k > TOPK_KC;  // no MFMA pre-selection: exact full scan of every row
   TRYC(set_device(c));
   const int src = side, dst = 1 - side;
   TRYC(materialize(c, src));
@@ -1129,17 +1138,21 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
     a.out_ids = d_oid.as<int32_t>();
     a.out_scores = d_osc.as<float>();
     a.need_exact = d_need.as<int32_t>();
-    HIPCHK(launch_topk(KP, a, c->st));
-    std::vector<int32_t> need(nc);
-    HIPCHK(hipMemcpyAsync(need.data(), d_need.p, nc * 4, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
-    std::vector<int32_t> flagged;
-    for (int64_t i = 0; i < nc; ++i)
-      if (need[i]) flagged.push_back((int32_t)i);
-    if (!flagged.empty()) {
-      HIPCHK(d_flag.ensure(flagged.size() * 4));
-      HIPCHK(hipMemcpy(d_flag.p, flagged.data(), flagged.size() * 4, hipMemcpyHostToDevice));
-      HIPCHK(launch_topk_exact(KP, a, d_flag.as<int32_t>(), (int64_t)flagged.size(), c->st));
+    if (exact_only) {
+      HIPCHK(launch_topk_exact(KP, a, nullptr, nc, c->st));
+    } else {
+      HIPCHK(launch_topk(KP, a, c->st));
+      std::vector<int32_t> need(nc);
+      HIPCHK(hipMemcpyAsync(need.data(), d_need.p, nc * 4, hipMemcpyDeviceToHost, c->st));
+      HIPCHK(hipStreamSynchronize(c->st));
+      std::vector<int32_t> flagged;
+      for (int64_t i = 0; i < nc; ++i)
+        if (need[i]) flagged.push_back((int32_t)i);
+      if (!flagged.empty()) {
+        HIPCHK(d_flag.ensure(flagged.size() * 4));
+        HIPCHK(hipMemcpy(d_flag.p, flagged.data(), flagged.size() * 4, hipMemcpyHostToDevice));
+        HIPCHK(launch_topk_exact(KP, a, d_flag.as<int32_t>(), (int64_t)flagged.size(), c->st));
+      }
     }
     std::vector<int32_t> oid(nc * k);
     std::vector<float> osc(nc * k);
@@ -1225,6 +1238,12 @@ int als_last_timings(const als_ctx* c, int dst_side, double* out, int n) {
 int als_path_stats(const als_ctx* c, int dst_side, int64_t* out4) {
   if (!c || (dst_side != 0 && dst_side != 1) || !out4) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
   for (int i = 0; i < 4; ++i) out4[i] = c->s[dst_side].stats[i];
+  return ALS_OK;
+}
+
+int als_solver_stats(const als_ctx* c, int dst_side, int64_t* out4) {
+  if (!c || (dst_side != 0 && dst_side != 1) || !out4) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  for (int i = 0; i < 4; ++i) out4[i] = c->s[dst_side].solver[i];
   return ALS_OK;
 }
 

@@ -1131,7 +1131,8 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
   __syncthreads();
   int phase = 0, last_wall = 0;
   const int iter_max = 400 > 20 * a.kreal ? 400 : 20 * a.kreal;
-  for (int iterno = 0; iterno < iter_max; ++iterno) {
+  int iterno = 0;
+  for (; iterno < iter_max; ++iterno) {
     if (iterno > 0 && (iterno & 63) == 0) axi = own ? sym_gemv_row<KP>(smem, vx, i) : 0.0;
     // residual = A x - b ; projected gradient
     const double res = own ? axi - bi : 0.0;
@@ -1189,6 +1190,10 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
   }
   if (own) a.X[(int64_t)j * KP + i] = i < a.kreal ? (float)xi : 0.f;
   if (tid == 0 && s_flag[1]) atomicOr(a.err, s_flag[1]);
+  if (tid == 0 && a.iters) {
+    atomicAdd(&a.iters[0], (unsigned long long)iterno);
+    atomicMax(&a.iters[1], (unsigned long long)iterno);
+  }
 }
 
 template <int KP>
@@ -1699,37 +1704,63 @@ __global__ __launch_bounds__(256) void topk_rescore_kernel(TopkArgs a) {
   }
 }
 
-// Exact fallback: one workgroup (4 waves) per flagged src row; full F2J scan with a wave-level
-// running top-64 per wave, merged at the end.
-template <int KP>
+// Exact path: one workgroup (4 waves) per src row, full F2J scan.  Each wave keeps its best 64·P
+// (score desc, id asc) in registers, slots [0, P) sorted, and buffers up to 64·P newcomers in slots
+// [P, 2P); a batch of 64 scores is only buffered when one of them reaches the current 64·P-th best,
+// and a full buffer is merged by one bitonic sort of the 128·P slots.  The four waves' lists are
+// merged at the end.  P = 1 serves the rows the MFMA pre-selection could not certify; P up to 8
+// serves k up to 512 (recommendForAll* with k > 64, no pre-selection).
+template <int KP, int P>
 __global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32_t* rows) {
-  __shared__ float msc[4][64];
-  __shared__ int mix[4][64];
+  __shared__ float msc[4][64 * P];
+  __shared__ int mix[4][64 * P];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t si = rows[blockIdx.x];
+  const int64_t si = rows ? rows[blockIdx.x] : (int64_t)blockIdx.x;
   const int srow = a.src_rows[si];
   const float* s = a.S + (int64_t)srow * KP;
-  float bs[2] = {-INFINITY, -INFINITY};
-  int bi[2] = {-1, -1};
+  float bs[2 * P];
+  int bi[2 * P];
+#pragma unroll
+  for (int h = 0; h < 2 * P; ++h) { bs[h] = -INFINITY; bi[h] = -1; }
+  int nin = 0;                // newcomer batches buffered (wave-uniform)
+  float thr = -INFINITY;      // the kept list's last score once full
   for (int64_t j0 = (int64_t)wave * 64; j0 < a.n_dst; j0 += 256) {
     const int64_t dj = j0 + lane;
-    bs[1] = dj < a.n_dst ? f2j_dot(s, a.T + dj * KP, a.kreal) : -INFINITY;
-    bi[1] = dj < a.n_dst ? (int)dj : -1;
-    wave_bitonic<2>(bs, bi);  // keeps the best 64 in bs[0]
-  }
-  msc[wave][lane] = bs[0];
-  mix[wave][lane] = bi[0];
-  __syncthreads();
-  if (wave == 0) {
-    float s4[4];
-    int i4[4];
+    const float sc = dj < a.n_dst ? f2j_dot(s, a.T + dj * KP, a.kreal) : -INFINITY;
+    if (!__any(sc >= thr)) continue;
+    static_for<0, P>([&](auto hh) {
+      constexpr int h = decltype(hh)::value;
+      if (nin == h) { bs[P + h] = sc; bi[P + h] = dj < a.n_dst ? (int)dj : -1; }
+    });
+    if (++nin == P) {
+      wave_bitonic<2 * P>(bs, bi);
 #pragma unroll
-    for (int h = 0; h < 4; ++h) { s4[h] = msc[h][lane]; i4[h] = mix[h][lane]; }
-    wave_bitonic<4>(s4, i4);
-    if (lane < a.k) {
-      const int idx = i4[0];
-      a.out_ids[si * a.k + lane] = idx >= 0 ? a.dst_ids[idx] : -1;
-      a.out_scores[si * a.k + lane] = idx >= 0 ? s4[0] : __int_as_float(0x7fc00000);
+      for (int h = P; h < 2 * P; ++h) { bs[h] = -INFINITY; bi[h] = -1; }
+      nin = 0;
+      thr = rdlane(bs[P - 1], 63);
+    }
+  }
+  wave_bitonic<2 * P>(bs, bi);
+#pragma unroll
+  for (int h = 0; h < P; ++h) {
+    msc[wave][64 * h + lane] = bs[h];
+    mix[wave][64 * h + lane] = bi[h];
+  }
+  __syncthreads();
+  if (wave == 0) {  // fold the other waves' lists in, one bitonic sort of 128·P slots each
+    for (int w = 1; w < 4; ++w) {
+#pragma unroll
+      for (int h = 0; h < P; ++h) { bs[P + h] = msc[w][64 * h + lane]; bi[P + h] = mix[w][64 * h + lane]; }
+      wave_bitonic<2 * P>(bs, bi);
+    }
+#pragma unroll
+    for (int h = 0; h < P; ++h) {
+      const int e = 64 * h + lane;
+      if (e < a.k) {
+        const int idx = bi[h];
+        a.out_ids[si * a.k + e] = idx >= 0 ? a.dst_ids[idx] : -1;
+        a.out_scores[si * a.k + e] = idx >= 0 ? bs[h] : __int_as_float(0x7fc00000);
+      }
     }
   }
 }
@@ -1775,13 +1806,25 @@ hipError_t launch_rownorm_max(const float* T, int64_t n, int KP, int kreal, unsi
   return hipGetLastError();
 }
 
+template <int KP, int P>
+hipError_t topk_exact_p(const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s) {
+  topk_exact_kernel<KP, P><<<(int)n_rows, 256, 0, s>>>(a, rows);
+  return hipGetLastError();
+}
+template <int KP>
+hipError_t topk_exact_kp(const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s) {
+  if (a.k <= 64) return topk_exact_p<KP, 1>(a, rows, n_rows, s);
+  if (a.k <= 128) return topk_exact_p<KP, 2>(a, rows, n_rows, s);
+  if (a.k <= 256) return topk_exact_p<KP, 4>(a, rows, n_rows, s);
+  if (a.k <= TOPK_MAX) return topk_exact_p<KP, 8>(a, rows, n_rows, s);
+  return hipErrorInvalidValue;
+}
 hipError_t launch_topk_exact(int KP, const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s) {
   if (n_rows <= 0) return hipSuccess;
-  if (KP == 64) topk_exact_kernel<64><<<(int)n_rows, 256, 0, s>>>(a, rows);
-  else if (KP == 128) topk_exact_kernel<128><<<(int)n_rows, 256, 0, s>>>(a, rows);
-  else if (KP == 256) topk_exact_kernel<256><<<(int)n_rows, 256, 0, s>>>(a, rows);
-  else return hipErrorInvalidValue;
-  return hipGetLastError();
+  if (KP == 64) return topk_exact_kp<64>(a, rows, n_rows, s);
+  if (KP == 128) return topk_exact_kp<128>(a, rows, n_rows, s);
+  if (KP == 256) return topk_exact_kp<256>(a, rows, n_rows, s);
+  return hipErrorInvalidValue;
 }
 
 }  // namespace albedo

@@ -25,6 +25,7 @@ struct SolveArgs {
   int* err;                // device flag: set to 1 when a solve meets a non-positive pivot
   const float* colscale;   // [2*KP] heavy-build fp16 column scales 2^e and their inverses
   const float* prebuilt;   // split rows: reduced A' records [n_rows][split_rec_floats] (else null)
+  unsigned long long* iters;  // NNLS: [0] += iterations of every row, [1] = max over rows (or null)
 };
 
 // Split-K of the heavy tail (rows with more ratings than one chunk): every chunk of chunk_len
@@ -98,12 +99,14 @@ struct TopkArgs {
   int32_t* need_exact;     // [n_src] set when the candidate set could not be certified
 };
 hipError_t launch_topk(int KP, const TopkArgs& a, hipStream_t s);
+// exact full scan for the given src-row indices (rows == null: rows 0 .. n_rows-1), any k <= TOPK_MAX
 hipError_t launch_topk_exact(int KP, const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s);
 // out[r] = (hi, lo) fp16 split of T[r]·scale: [n][2*KP] halves (scale a power of two)
 hipError_t launch_split_rows(const float* T, int64_t n, int KP, float scale, void* out, hipStream_t s);
 // *out = bits of max_r ||T[r][0..kreal)||_2 computed in fp64
 hipError_t launch_rownorm_max(const float* T, int64_t n, int KP, int kreal, unsigned long long* out, hipStream_t s);
-constexpr int TOPK_KC = 64;  // candidates kept per src row by the MFMA pass
+constexpr int TOPK_KC = 64;     // candidates kept per src row by the MFMA pass (k <= 64)
+constexpr int TOPK_MAX = 512;   // k above TOPK_KC: exact full scan (topk_exact_kernel)
 
 // Ingest (ingest.hip): COO -> remap + CSR.
 struct DeviceBuf;
@@ -112,6 +115,14 @@ hipError_t remap_ids(const int32_t* d_ids, int64_t n, int32_t* d_dense, int32_t*
 hipError_t build_csr(const int32_t* d_dst, const int32_t* d_src, const float* d_val, int64_t n,
                      int64_t n_dst, int64_t n_src, int64_t* d_ptr, int32_t* d_col, float* d_valout,
                      hipStream_t s);
+// Shard row starts of one side (world + 1 entries, world <= 16), passed by value to kernels.
+struct ShardStarts {
+  int64_t s[17];
+  int world;
+};
+// out[e] = padded all-gather position of dense src row in[e] (rank r's rows start at r * maxrows)
+hipError_t padded_remap(const int32_t* d_in, int64_t n, const ShardStarts& st, int64_t maxrows, int32_t* d_out,
+                        hipStream_t s);
 // Synthetic generator (synth.hip)
 hipError_t synth_fill(uint64_t seed, int rounds, int64_t n_users, int64_t n_items,
                       const int64_t* d_deg_prefix, const double* d_cw, const int32_t* d_perm,

@@ -16,7 +16,10 @@ import numpy as np
 def into_user_items(user, item, key, k):
     user = np.asarray(user)
     item = np.asarray(item)
-    key = np.asarray(key, dtype=np.float64)
+    key = np.asarray(key)
+    if key.dtype.kind == "M":  # timestamps (starred_at read from parquet)
+        key = key.astype("datetime64[us]").astype(np.int64)
+    key = key.astype(np.float64)
     order = np.lexsort((item, -key, user))
     u, it, ky = user[order], item[order], key[order]
     if u.size == 0:

@@ -25,3 +25,8 @@ def today() -> str:
 def als_model_path() -> str:
     """ALSRecommenderBuilder.scala:44 / ALSRecommender.scala:17."""
     return f"{data_dir()}/{today()}/alsModel.parquet"
+
+
+def raw_starring_path() -> str:
+    """DatasetUtils.scala:114 (loadRawStarringDS's parquet cache)."""
+    return f"{data_dir()}/{today()}/rawStarringDF.parquet"

@@ -120,8 +120,14 @@ def main():
         stage[0] += tt
     barrier()
     elapsed = time.perf_counter() - t_start
+    nnls_iters = {}
     for side in (0, 1):
         L.check(lib.als_path_stats(h, side, L.ptr(stats[side], C.c_int64)))
+        if args.config in NONNEGATIVE:
+            sv = np.zeros(4, np.int64)
+            L.check(lib.als_solver_stats(h, side, L.ptr(sv, C.c_int64)))
+            nnls_iters["user" if side == 0 else "item"] = {"mean": float(sv[0]) / max(int(sv[2]), 1),
+                                                            "max": int(sv[1]), "rows": int(sv[2])}
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -197,6 +203,7 @@ def main():
             "stages_ms_per_sweep": {f"{'user' if s == 0 else 'item'}_{n}": round((stage[s][i] / args.steps), 3)
                                     for s in (0, 1) for i, n in enumerate(L.T_NAMES[:7])},
             "paths": {"user": stats[0].tolist(), "item": stats[1].tolist()},
+            "nnls_iterations_last_sweep": nnls_iters or None,
             "setup_s": setup_s,
         }
         print(json.dumps(line), flush=True)

@@ -133,7 +133,9 @@ int als_model_create(int32_t rank, int64_t n_users, const int32_t* user_ids, con
  * for each requested src id (all src rows when subset==NULL, ascending) the top-k dst ids by the
  * F2J-order fp32 dot product (ALSRecommender.scala:51), sorted (score desc, id asc).
  * Outputs [n_src][k]; rows with fewer than k dst entries are padded with id -1 / score NaN.
- * Unknown subset ids produce an all-padding row.  src_ids_out may be NULL. */
+ * Unknown subset ids produce an all-padding row.  src_ids_out may be NULL.
+ * k <= 64: MFMA pre-selection + exact rescoring; 64 < k <= 512: exact full scan per src row (slower);
+ * k > 512: ALS_E_UNSUPPORTED. */
 int als_recommend(als_ctx* ctx, int side, int32_t k, const int32_t* subset, int64_t n_subset,
                   int32_t* src_ids_out, int32_t* dst_ids_out, float* scores_out);
 /* ALSModel.transform: F2J sdot per (user, item) pair; NaN when either id is unknown. */
@@ -149,6 +151,9 @@ int als_last_timings(const als_ctx* ctx, int dst_side, double* out, int n);
 /* Rows / nnz handled by each solve path in the last half-sweep of dst_side:
  * out[0]=light rows, out[1]=light nnz, out[2]=heavy rows, out[3]=heavy nnz. */
 int als_path_stats(const als_ctx* ctx, int dst_side, int64_t* out4);
+/* NNLS iteration counts of the last half-sweep of dst_side (nonnegative = true):
+ * out[0] = iterations summed over rows, out[1] = max over rows, out[2] = rows, out[3] = 0. */
+int als_solver_stats(const als_ctx* ctx, int dst_side, int64_t* out4);
 /* Synchronise the context's streams (bench barrier helper). */
 int als_synchronize(als_ctx* ctx);
 

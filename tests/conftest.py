@@ -22,3 +22,9 @@ def gpu_lib():
     n = _lib.device_count()
     assert n > 0, "no gfx950 device visible to libalbedo_als.so"
     return lib
+
+
+@pytest.fixture(autouse=True)
+def _isolated_data_dir(tmp_path, monkeypatch):
+    """albedo's date-keyed caches (settings.data_dir) live in the test's own directory."""
+    monkeypatch.setenv("ALBEDO_DATA_DIR", str(tmp_path / "spark-data"))

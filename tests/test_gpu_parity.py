@@ -364,6 +364,36 @@ def test_topk_large_catalogue_bit_exact(gpu_lib, rank, num):
         gpu_lib.als_destroy(h)
 
 
+@pytest.mark.parametrize("num", [100, 300])
+def test_topk_above_64_exact_scan(gpu_lib, num):
+    """k > 64 (Spark's recommendForAllUsers takes any k): exact full-scan path, ids and F2J score
+    bits against the oracle, ties included; k above the engine's 512 raises."""
+    from albedo_amd import _lib as L
+    rng = np.random.default_rng(num)
+    n_u, n_i, rank = 70, 5003, 40
+    uid = np.arange(n_u, dtype=np.int32) * 5 + 1
+    iid = rng.permutation(np.arange(n_i, dtype=np.int32) * 3 + 2).astype(np.int32)
+    uf = rng.standard_normal((n_u, rank)).astype(np.float32)
+    itf = rng.standard_normal((n_i, rank)).astype(np.float32)
+    itf[2500:2600] = itf[:100]  # exact ties
+    h = C.c_void_p()
+    L.check(gpu_lib.als_model_create(rank, n_u, L.ptr(uid, C.c_int32), L.ptr(uf, C.c_float), n_i,
+                                     L.ptr(iid, C.c_int32), L.ptr(itf, C.c_float), -1, C.byref(h)))
+    try:
+        ids = np.empty((n_u, num), np.int32)
+        sc = np.empty((n_u, num), np.float32)
+        L.check(gpu_lib.als_recommend(h, 0, num, None, n_u, None, L.ptr(ids, C.c_int32), L.ptr(sc, C.c_float)))
+        ref_ids, ref_sc = O.recommend_for_all(uid, uf, iid, itf, num)
+        assert np.array_equal(ids, ref_ids)
+        assert np.array_equal(sc.view(np.uint32), ref_sc.view(np.uint32))
+        big = np.empty((n_u, 513), np.int32)
+        with pytest.raises(L.ALSError, match="not supported"):
+            L.check(gpu_lib.als_recommend(h, 0, 513, None, n_u, None, L.ptr(big, C.c_int32),
+                                          L.ptr(np.empty((n_u, 513), np.float32), C.c_float)))
+    finally:
+        gpu_lib.als_destroy(h)
+
+
 def test_topk_subset_unknown_ids_and_small_catalogue(gpu_lib):
     from albedo_amd import _lib as L
     rng = np.random.default_rng(7)

@@ -51,18 +51,22 @@ def _problem():
     return B, U0, V0
 
 
-def test_sharded_layout_cpu_world2(tmp_path):
-    """Shard planner + padded all-gather layout reproduce the single-process half-sweep."""
-    res = _launch("cpu", str(tmp_path / "cpu.npz"))
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_layout_cpu(tmp_path, world):
+    """Shard planner + padded all-gather layout reproduce the single-process half-sweep (world 3:
+    uneven shards, padded rows in the gathered layout)."""
+    res = _launch("cpu", str(tmp_path / "cpu.npz"), world=world)
     B, U0, _ = _problem()
     V = O.half_sweep(U0, B.i_ptr, B.i_col, B.i_val, reg=0.5, alpha=40.0)
     assert np.allclose(res["V"], V, rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.gpu
-def test_sharded_fit_gpu_world2_matches_single(gpu_lib, tmp_path):
-    """Two ranks (sharing the box's GPU) run the engine's sharded fit; factors match one rank."""
-    res = _launch("gpu", str(tmp_path / "gpu.npz"))
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_fit_gpu_matches_single(gpu_lib, tmp_path, world):
+    """Ranks sharing the box's GPU run the engine's sharded fit (device padded remap, host
+    transport for the Gram all-reduce and the factor all-gather); factors match one rank."""
+    res = _launch("gpu", str(tmp_path / "gpu.npz"), world=world)
     B, U0, V0 = _problem()
     U, V = O.fit(B, rank=16, max_iter=3, reg=0.5, alpha=40.0, init_user=U0, init_item=V0)
     rel = lambda a, b: np.max(np.abs(a - b)) / np.max(np.abs(b))

@@ -22,7 +22,8 @@ def per_kernel(path, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("albedo::", "")
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+            k = k.replace("void ", "").replace("albedo::", "")
             base = k.split("<")[0].replace("_kernel", "")
             tot[base] += float(r["Counter_Value"])
             nd[base].add(r["Dispatch_Id"])
@@ -37,7 +38,7 @@ def main():
                       "--steps 1 --warmup 0 --no-cpu --topk-users 0`; FETCH_SIZE x2 (gfx950 wide-read correction); "
                       "GB (1e9 B) per sweep, summed over the kernel's launches"}
     for k in sorted(set(fetch) | set(write)):
-        if not k.startswith(("solve_", "gram", "rotate", "topk")):
+        if not k.startswith(("solve_", "gram", "rotate", "topk", "heavy_")):
             continue
         f_gb = 2.0 * fetch.get(k, 0.0) * 1024 / 1e9
         w_gb = write.get(k, 0.0) * 1024 / 1e9
