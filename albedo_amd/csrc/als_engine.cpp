@@ -461,7 +461,7 @@ int half_sweep_nnls(als_ctx* c, int t) {
       for (int j = 0; j < k; ++j) S.G[(size_t)i * k + j] = Gf[(size_t)i * KP + j];
     S.GB = S.B;
     for (int i = 0; i < KP; ++i)
-      for (int j = 0; j <= i; ++j) gt[nnls_gtile_index(i, j)] = (float)Gf[(size_t)i * KP + j];
+      for (int j = 0; j < 16 * ((i >> 4) + 1); ++j) gt[nnls_gtile_index(i, j)] = (float)Gf[(size_t)i * KP + j];
   }
   HIPCHK(hipEventRecord(ev[1], st));
   HIPCHK(c->d_Gt.ensure((size_t)ngt * 4));

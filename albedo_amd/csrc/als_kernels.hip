@@ -528,6 +528,12 @@ hipError_t launch_solve_light(int KP, int D, const SolveArgs& a, hipStream_t s) 
 constexpr int HT_LD = 17, HT_SZ = 16 * HT_LD;
 __device__ __forceinline__ int htile(int I, int J) { return (I * (I + 1) / 2 + J) * HT_SZ; }
 __device__ __forceinline__ int hel(int r, int c) { return htile(r >> 4, c >> 4) + (r & 15) * HT_LD + (c & 15); }
+// NNLS layout: packed lower 16x16 tiles with 16-float rows (1 KiB per tile, 16-B aligned rows for
+// ds_read_b128), diagonal tiles stored full (both triangles)
+__host__ __device__ __forceinline__ constexpr int ntile(int I, int J) { return (I * (I + 1) / 2 + J) * 256; }
+__host__ __device__ __forceinline__ constexpr int nel(int r, int c) {
+  return ntile(r >> 4, c >> 4) + (r & 15) * 16 + (c & 15);
+}
 
 
 template <int KP>
@@ -566,7 +572,7 @@ __device__ __forceinline__ uint32_t pack_h2(float a, float b) {
 
 // Build of the row's A' tiles owned by this wave: row blocks rb .. rb+NR-1, column blocks
 // cb .. cb+GS-1 (DIAG: the same blocks, upper tiles only).
-template <int KP, bool DIAG>
+template <int KP, bool DIAG, bool NT = false>
 __device__ __forceinline__ void heavy_build(const SolveArgs& a, int64_t p0, int d, float* smem, int rb, int cb) {
   using H = Heavy<KP>;
   constexpr int NR = DIAG ? H::GS : H::GS / 2, NC = H::GS, NST = H::NST;
@@ -733,7 +739,13 @@ __device__ __forceinline__ void heavy_build(const SolveArgs& a, int64_t p0, int 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int c1 = 16 * (rb + i) + 4 * g + r, c2 = 16 * (cb + j) + i16;
-        if (!DIAG || i != j || c1 >= c2) smem[c1 >= c2 ? hel(c1, c2) : hel(c2, c1)] = acc[t][r] * ir[r] * ic;
+        const float v = acc[t][r] * ir[r] * ic;
+        if constexpr (NT) {  // NNLS layout: diagonal tiles full
+          smem[c1 >= c2 ? nel(c1, c2) : nel(c2, c1)] = v;
+          if (DIAG && i == j) smem[nel(c2, c1)] = v;
+        } else if (!DIAG || i != j || c1 >= c2) {
+          smem[c1 >= c2 ? hel(c1, c2) : hel(c2, c1)] = v;
+        }
       }
     }
   }
@@ -741,18 +753,18 @@ __device__ __forceinline__ void heavy_build(const SolveArgs& a, int64_t p0, int 
 
 // Dispatch of the build over the waves: waves 0..NG-1 own the diagonal group pairs, the rest
 // split each off-diagonal group pair (gi < gj) into two halves of its row blocks.
-template <int KP>
+template <int KP, bool NT = false>
 __device__ __forceinline__ void heavy_build_all(const SolveArgs& a, int64_t p0, int d, float* smem) {
   using H = Heavy<KP>;
   const int wave = threadIdx.x >> 6;
   if (wave < H::NG) {
-    heavy_build<KP, true>(a, p0, d, smem, wave * H::GS, wave * H::GS);
+    heavy_build<KP, true, NT>(a, p0, d, smem, wave * H::GS, wave * H::GS);
   } else {
     const int idx = wave - H::NG, pair = idx >> 1, half = idx & 1;
     int gi = 0, gj = 1;
     for (int p = 0; p < pair; ++p)
       if (++gj == H::NG) { ++gi; gj = gi + 1; }
-    heavy_build<KP, false>(a, p0, d, smem, gi * H::GS + half * (H::GS / 2), gj * H::GS);
+    heavy_build<KP, false, NT>(a, p0, d, smem, gi * H::GS + half * (H::GS / 2), gj * H::GS);
   }
   __syncthreads();
 }
@@ -1025,151 +1037,238 @@ __global__ __launch_bounds__(Heavy<KP>::NTH, 4) void solve_heavy_kernel(SolveArg
 // the heavy rows (same LDS stage + MFMA + packed tiles) plus the G tiles, then Spark's projected
 // gradient with CG acceleration, thread i = coordinate i, fp64 vectors and block reductions.
 // =============================================================================================
-template <int NW, int N>
-__device__ __forceinline__ void block_sum(double (&v)[N], double* scr, int& phase) {
+// Block reductions of the NNLS loop.  Only the NO = KP/64 waves that own coordinates hold nonzero
+// terms, so only they reduce (wave-level DPP/shuffle sums, one partial per wave in LDS); after the
+// barrier every wave reads the NO partials (uniform control flow needs the result everywhere).
+template <int NO, int N>
+__device__ __forceinline__ void own_sum(double (&v)[N], double* scr, int& phase) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double* sp = scr + phase * 16 * 8;
+  if (wave < NO) {
 #pragma unroll
-  for (int n = 0; n < N; ++n)
-    for (int o = 32; o > 0; o >>= 1) v[n] += __shfl_xor(v[n], o);
-  double* sp = scr + phase * NW * 8;
-  if (lane == 0) {
+    for (int n = 0; n < N; ++n)
+      for (int o = 32; o > 0; o >>= 1) v[n] += __shfl_xor(v[n], o);
+    if (lane == 0) {
 #pragma unroll
-    for (int n = 0; n < N; ++n) sp[wave * 8 + n] = v[n];
+      for (int n = 0; n < N; ++n) sp[n * 16 + wave] = v[n];
+    }
   }
   __syncthreads();
 #pragma unroll
   for (int n = 0; n < N; ++n) {
-    double s = sp[n];
-    for (int w = 1; w < NW; ++w) s += sp[8 * w + n];
-    v[n] = s;
+    double t = sp[n * 16];
+#pragma unroll
+    for (int w = 1; w < NO; ++w) t += sp[n * 16 + w];
+    v[n] = t;
   }
   phase ^= 1;
 }
 
-template <int NW>
-__device__ __forceinline__ double block_min(double v, double* scr, int& phase) {
+template <int NO>
+__device__ __forceinline__ double own_min(double v, double* scr, int& phase) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
-  double* sp = scr + phase * NW * 8;
-  if (lane == 0) sp[wave * 8] = v;
+  double* sp = scr + phase * 16 * 8;
+  if (wave < NO) {
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    if (lane == 0) sp[wave] = v;
+  }
   __syncthreads();
   v = sp[0];
-  for (int w = 1; w < NW; ++w) v = fmin(v, sp[8 * w]);
+#pragma unroll
+  for (int w = 1; w < NO; ++w) v = fmin(v, sp[w]);
   phase ^= 1;
   return v;
 }
 
-// (A v)_i for the symmetric matrix held as packed lower tiles; vec in LDS (fp64)
-template <int KP>
-__device__ __forceinline__ double sym_gemv_row(const float* smem, const double* vec, int i) {
-  const int I = i >> 4, ii = i & 15;
-  double acc = 0.0;
-  for (int J = 0; J < I; ++J) {  // row i, tiles left of the diagonal
-    const float* r = smem + htile(I, J) + ii * HT_LD;
+// y = A·v for NV vectors at once (A symmetric, NNLS layout: packed lower 16x16 tiles, diagonal
+// tiles full; v and y fp32 in LDS).  Wave w takes the row blocks I = w, w + NW, ...; lane l reads
+// 16 B of tile row r = l >> 2 (columns 4q .. 4q+3, q = l & 3) per tile with ds_read_b128, so one
+// pass over a row block streams each of its 16x16 tiles once:
+//   J <= I   stored tile (I, J):    y_I[r]      += Σ_s T[r][4q+s] v_J[4q+s]    (sum over q)
+//   J >  I   stored tile (J, I)ᵀ:  y_I[4q+s]   += T[r][4q+s] v_J[r]           (sum over r)
+// Partial sums combine by DPP (quad_perm, row_ror) plus two cross-row shuffles, fp32 throughout.
+template <int CTRL>
+__device__ __forceinline__ float dppf(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, true));
+}
+
+// tid: threadIdx.x, passed through an empty asm by the caller every iteration so that the compiler
+// recomputes these LDS addresses instead of hoisting dozens of them out of the NNLS loop (which spills
+// at the 128 VGPRs a 1024-thread workgroup allows).
+template <int KP, int NV>
+__device__ __forceinline__ void nt_symv(const float* __restrict__ A, const float* const (&v)[2], float* const (&y)[2],
+                                        float* scratch /* per wave: NV x 16 floats */, int tid) {
+  constexpr int NB = KP / 16, NW = Heavy<KP>::NW;
+  const int lane = tid & 63, wave = tid >> 6, r = lane >> 2, q = lane & 3;
+  for (int I = wave; I < NB; I += NW) {
+    float yn[NV], yt[NV][4];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) acc += (double)r[c] * vec[16 * J + c];
-  }
-  {
-    const float* t = smem + htile(I, I);
+    for (int n = 0; n < NV; ++n) {
+      yn[n] = 0.f;
 #pragma unroll
-    for (int c = 0; c < 16; ++c) acc += (double)(c <= ii ? t[ii * HT_LD + c] : t[c * HT_LD + ii]) * vec[16 * I + c];
-  }
-  for (int J = I + 1; J < KP / 16; ++J) {  // column i of the tiles below the diagonal
-    const float* t = smem + htile(J, I) + ii;
+      for (int e = 0; e < 4; ++e) yt[n][e] = 0.f;
+    }
+#pragma unroll 2
+    for (int J = 0; J < NB; ++J) {
+      if (J <= I) {
+        const f32x4 t = ld4(A + ntile(I, J) + 16 * r + 4 * q);
 #pragma unroll
-    for (int c = 0; c < 16; ++c) acc += (double)t[c * HT_LD] * vec[16 * J + c];
+        for (int n = 0; n < NV; ++n) {
+          const f32x4 x = ld4(v[n] + 16 * J + 4 * q);
+          yn[n] = fmaf(t[0], x[0], fmaf(t[1], x[1], fmaf(t[2], x[2], fmaf(t[3], x[3], yn[n]))));
+        }
+      } else {
+        const f32x4 t = ld4(A + ntile(J, I) + 16 * r + 4 * q);
+#pragma unroll
+        for (int n = 0; n < NV; ++n) {
+          const float x = v[n][16 * J + r];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) yt[n][e] = fmaf(t[e], x, yt[n][e]);
+        }
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NV; ++n) {
+      yn[n] += dppf<0xB1>(yn[n]);  // quad_perm [1,0,3,2]: lanes 4r..4r+3 share row r
+      yn[n] += dppf<0x4E>(yn[n]);  // quad_perm [2,3,0,1]
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // sum over r: lanes q, q+4, ... of the 16-lane row, then the 4 rows
+        float x = yt[n][e];
+        x += dppf<0x124>(x);  // row_ror:4
+        x += dppf<0x128>(x);  // row_ror:8
+        x += __shfl_xor(x, 16);
+        x += __shfl_xor(x, 32);
+        yt[n][e] = x;
+      }
+      if (lane < 4) *reinterpret_cast<f32x4*>(scratch + 16 * n + 4 * lane) = f32x4{yt[n][0], yt[n][1], yt[n][2], yt[n][3]};
+    }
+    WAVE_LDS_SYNC();
+    if (q == 0) {
+#pragma unroll
+      for (int n = 0; n < NV; ++n) y[n][16 * I + r] = yn[n] + scratch[16 * n + r];
+    }
+    WAVE_LDS_SYNC();
   }
-  return acc;
 }
 
 template <int KP>
 struct NnlsLds {
   static constexpr int NW = Heavy<KP>::NW;
   static constexpr int BASE = Heavy<KP>::FLOATS;           // heavy layout first (tiles, b', flags)
-  static constexpr int OFF_V = (BASE + 1) & ~1;            // fp64 vectors: x, grad, dir (KP each)
-  static constexpr int OFF_SCR = OFF_V + 2 * 3 * KP;       // fp64 reduction scratch [2][NW][8]
-  static constexpr int FLOATS = OFF_SCR + 2 * 2 * NW * 8;
+  static constexpr int OFF_V = (BASE + 3) & ~3;            // fp32 vectors: product inputs v0, v1
+  static constexpr int OFF_Y = OFF_V + 2 * KP;             // fp32 products y0, y1
+  static constexpr int OFF_W = OFF_Y + 2 * KP;             // per-wave product scratch [NW][32]
+  static constexpr int OFF_SCR = (OFF_W + 32 * NW + 1) & ~1;  // fp64 reduction scratch [2][8][16]
+  static constexpr int FLOATS = OFF_SCR + 2 * 2 * 8 * 16;
+  static_assert(ntile(KP / 16, 0) <= Heavy<KP>::OFF_B, "NNLS tiles fit where the heavy build leaves its tiles");
 };
 
 __device__ __forceinline__ bool nnls_stop(double step, double ndir, double nx) {
   return isnan(step) || step < 1e-7 || step > 1e40 || ndir < 1e-12 * nx || ndir < 1e-32;
 }
 
+// NNLS rows (nonnegative = true; Spark NNLSSolver -> mllib/optimization/NNLS.scala).  Original basis
+// (the constraints are coordinate-wise): A = G + λn I + Σ c y yᵀ built like the heavy rows (same LDS
+// stage + MFMA) into the NNLS tile layout, then Spark's projected gradient with CG acceleration:
+// thread i < KP owns coordinate i (x, residual, directions in fp64 registers), every wave takes part
+// in the products.  Per iteration ONE pass over A yields A·grad and A·dir together (dir = grad +
+// alpha·lastDir is known once ‖grad‖² is reduced), and the residual follows the steps
+// (A·x_new = A·x - step·A·dir, exact refresh every 64 iterations): Spark's three products become one
+// pass.  Stopping rules, the wall clamp and the CG restarts are Spark's, unchanged.
 template <int KP, bool PRE = false>
 __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a, const float* __restrict__ Gt) {
   using H = Heavy<KP>;
   using NL = NnlsLds<KP>;
-  constexpr int NTL = H::NTL, NTH = H::NTH, NW = H::NW;
+  constexpr int NTH = H::NTH, NB = KP / 16, NTT = NB * (NB + 1) / 2 * 256, NO = KP / 64;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* bvec = smem + H::OFF_B;
   int* s_flag = reinterpret_cast<int*>(smem + H::OFF_FLAG);
-  double* vx = reinterpret_cast<double*>(smem + NL::OFF_V);
-  double* vg = vx + KP;
-  double* vd = vg + KP;
+  float* v0 = smem + NL::OFF_V;
+  float* v1 = v0 + KP;
+  float* y0 = smem + NL::OFF_Y;
+  float* y1 = y0 + KP;
   double* scr = reinterpret_cast<double*>(smem + NL::OFF_SCR);
+  const float* const vv[2] = {v0, v1};
+  float* const yy[2] = {y0, y1};
   const int tid = threadIdx.x;
   const int j = a.rows[blockIdx.x];
   const int64_t p0 = a.ptr[j];
   const int d = (int)(a.ptr[j + 1] - p0);
   if (tid == 0) { s_flag[0] = 0; s_flag[1] = 0; }
-  if constexpr (PRE) heavy_load_record<KP>(a.prebuilt + (size_t)blockIdx.x * SplitRec<KP>::FLOATS, smem);
-  else heavy_build_all<KP>(a, p0, d, smem);
+  if constexpr (PRE) {  // split row: the reduced record (heavy tile layout) -> NNLS layout
+    const float* rec = a.prebuilt + (size_t)blockIdx.x * SplitRec<KP>::FLOATS;
+    for (int e = tid; e < NTT; e += NTH) {
+      const int t = e >> 8, w = e & 255, rr = w >> 4, cc = w & 15;
+      int I = 0;
+      while ((I + 1) * (I + 2) / 2 <= t) ++I;
+      const bool diag = t == I * (I + 1) / 2 + I;
+      smem[e] = (diag && cc > rr) ? rec[t * HT_SZ + cc * HT_LD + rr] : rec[t * HT_SZ + rr * HT_LD + cc];
+    }
+    for (int c = tid; c < KP; c += NTH) bvec[c] = rec[SplitRec<KP>::OFF_B + c];
+    if (tid == 0) s_flag[0] = reinterpret_cast<const int*>(rec)[SplitRec<KP>::OFF_N];
+    __syncthreads();
+  } else {
+    heavy_build_all<KP, true>(a, p0, d, smem);
+  }
   const float lamn = a.reg * (float)(a.implicit ? s_flag[0] : d);
-  for (int e = tid; e < NTL * HT_SZ; e += NTH) smem[e] += Gt[e];   // A = G + Σ c y yᵀ
+  for (int e = tid; e < NTT; e += NTH) smem[e] += Gt[e];  // A = G + Σ c y yᵀ (Gt: the same layout)
   __syncthreads();
-  for (int c = tid; c < KP; c += NTH) smem[hel(c, c)] += c < a.kreal ? lamn : 1.0f;
+  for (int c = tid; c < KP; c += NTH) smem[nel(c, c)] += c < a.kreal ? lamn : 1.0f;
   const bool own = tid < KP;
   const int i = own ? tid : 0;
   const double bi = own ? (double)bvec[i] : 0.0;
-  // Two symmetric products per iteration instead of Spark's three (ata·x, ata·grad, ata·dir): the
-  // residual follows the steps, A·x_new = A·x - step·A·dir (a wall clamp moves x_i by <= 1e-14·x_i;
-  // x = 0 at the start gives A·x = 0), recomputed exactly every 64 iterations.  A·dir stays an
-  // explicit product: its recurrence A·grad + alpha·A·lastDir saves the product but, measured at c5,
-  // costs as many extra iterations (c5 sweep: 11.6 s Spark's three products, 7.6 s this, 7.5 s one).
   double xi = 0.0, axi = 0.0, last_dir = 0.0, last_norm = 0.0;
-  if (own) vx[i] = 0.0;
   __syncthreads();
   int phase = 0, last_wall = 0;
   const int iter_max = 400 > 20 * a.kreal ? 400 : 20 * a.kreal;
   int iterno = 0;
   for (; iterno < iter_max; ++iterno) {
-    if (iterno > 0 && (iterno & 63) == 0) axi = own ? sym_gemv_row<KP>(smem, vx, i) : 0.0;
+    int ot = tid;  // opaque copy of threadIdx.x (see nt_symv)
+    asm volatile("" : "+v"(ot));
+    float* const wsc = smem + NL::OFF_W + 32 * (ot >> 6);
+    if (iterno > 0 && (iterno & 63) == 0) {  // exact residual refresh: A·x
+      if (own) v0[i] = (float)xi;
+      __syncthreads();
+      nt_symv<KP, 1>(smem, vv, yy, wsc, ot);
+      __syncthreads();
+      if (own) axi = (double)y0[i];
+    }
     // residual = A x - b ; projected gradient
     const double res = own ? axi - bi : 0.0;
     double gi = res;
     if (gi > 0.0 && xi == 0.0) gi = 0.0;
-    if (own) vg[i] = gi;
+    double r1[3] = {gi * gi, gi * res, xi * xi};
+    own_sum<NO, 3>(r1, scr, phase);
+    const double ngrad = r1[0], nx = r1[2];
+    const bool cg = iterno > last_wall + 1;
+    const double dc = cg ? gi + (ngrad / last_norm) * last_dir : 0.0;
+    if (own) {
+      v0[i] = (float)gi;
+      v1[i] = (float)dc;
+    }
     __syncthreads();
-    const double agi = own ? sym_gemv_row<KP>(smem, vg, i) : 0.0;
-    double r1[4] = {gi * gi, gi * res, gi * agi, xi * xi};
-    block_sum<NW, 4>(r1, scr, phase);
-    const double ngrad = r1[0], nx = r1[3];
-    double step = r1[1] / (r1[2] + 1e-20);
-    double di = gi, adi = agi, ndir;
-    if (iterno > last_wall + 1) {
-      const double alpha = ngrad / last_norm;
-      const double dc = gi + alpha * last_dir;
-      if (own) vd[i] = dc;
-      __syncthreads();
-      const double adc = own ? sym_gemv_row<KP>(smem, vd, i) : 0.0;
-      double r2[3] = {dc * res, dc * adc, dc * dc};
-      block_sum<NW, 3>(r2, scr, phase);
-      const double dstep = r2[0] / (r2[1] + 1e-20);
-      if (nnls_stop(dstep, r2[2], nx)) {
-        ndir = ngrad;  // reject the CG direction
-      } else {
+    if (cg) nt_symv<KP, 2>(smem, vv, yy, wsc, ot);
+    else nt_symv<KP, 1>(smem, vv, yy, wsc, ot);
+    __syncthreads();
+    const double agi = own ? (double)y0[i] : 0.0;
+    const double adc = (own && cg) ? (double)y1[i] : 0.0;
+    double r2[4] = {gi * agi, dc * res, dc * adc, dc * dc};
+    own_sum<NO, 4>(r2, scr, phase);
+    double step = r1[1] / (r2[0] + 1e-20);
+    double di = gi, adi = agi, ndir = ngrad;
+    if (cg) {
+      const double dstep = r2[1] / (r2[2] + 1e-20);
+      if (!nnls_stop(dstep, r2[3], nx)) {  // else: reject the CG direction
         step = dstep;
         di = dc;
         adi = adc;
-        ndir = r2[2];
+        ndir = r2[3];
       }
-    } else {
-      ndir = ngrad;
     }
     if (nnls_stop(step, ndir, nx)) break;
     // don't run through the walls: step = min(step, x_i / d_i over d_i > 0 with step d_i > x_i)
     const double cand = (own && step * di > xi) ? xi / di : INFINITY;
-    step = fmin(step, block_min<NW>(cand, scr, phase));
+    step = fmin(step, own_min<NO>(cand, scr, phase));
     // take the step
     double hit = 0.0;
     if (own) {
@@ -1180,10 +1279,9 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
         xi -= step * di;
       }
       axi -= step * adi;
-      vx[i] = xi;
     }
     double r3[1] = {hit};
-    block_sum<NW, 1>(r3, scr, phase);
+    own_sum<NO, 1>(r3, scr, phase);
     if (r3[0] > 0.0) last_wall = iterno;
     last_dir = di;
     last_norm = ngrad;
@@ -1215,8 +1313,8 @@ hipError_t launch_solve_nnls(int KP, const SolveArgs& a, const float* Gt, hipStr
   if (KP == 256) return launch_nnls_kp<256>(a, Gt, s);
   return hipErrorInvalidValue;
 }
-int nnls_gtile_floats(int KP) { const int nb = KP / 16; return nb * (nb + 1) / 2 * HT_SZ; }
-int nnls_gtile_index(int r, int c) { return (r >> 4) * ((r >> 4) + 1) / 2 * HT_SZ + (c >> 4) * HT_SZ + (r & 15) * HT_LD + (c & 15); }
+int nnls_gtile_floats(int KP) { const int nb = KP / 16; return nb * (nb + 1) / 2 * 256; }
+int nnls_gtile_index(int r, int c) { return nel(r, c); }
 
 template <int KP>
 hipError_t launch_heavy_kp(const SolveArgs& a, hipStream_t s) {

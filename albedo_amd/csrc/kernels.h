@@ -61,7 +61,7 @@ hipError_t launch_solve_heavy(int KP, const SolveArgs& a, hipStream_t s);
 // heavy rows, one wave per row (heavy_wave.hip), KP <= 128; rows of any degree (split rows excepted)
 hipError_t launch_solve_wave(int KP, const SolveArgs& a, hipStream_t s);
 
-// nonnegative = true: Spark NNLS per row; Gt = the src Gram in packed lower 16x17 tiles (fp32).
+// nonnegative = true: Spark NNLS per row; Gt = the src Gram in the NNLS tile layout (fp32).
 hipError_t launch_solve_nnls(int KP, const SolveArgs& a, const float* Gt, hipStream_t s);
 int nnls_gtile_floats(int KP);
 // colscale[c] = 2^e_c with max_rows |Z[.][c]|·√cmax < 2^13, colscale[KP+c] = 2^-e_c (tmp: KP uints)
@@ -69,7 +69,7 @@ hipError_t launch_colscale(int KP, const float* Z, int64_t n, float cmax, unsign
                            hipStream_t s);
 // *out = bits of max |v[i]| (non-negative float, compared as unsigned)
 hipError_t launch_absmax(const float* v, int64_t n, unsigned* out, hipStream_t s);
-int nnls_gtile_index(int r, int c);  // r >= c
+int nnls_gtile_index(int r, int c);  // block(r) >= block(c): NNLS tile layout, diagonal tiles full
 
 // Seeded unit-norm Gaussian rows (global row index row0 + r) for large synthetic runs.
 hipError_t launch_init_random(int KP, int kreal, float* X, int64_t n, uint64_t seed, int64_t row0, hipStream_t s);
