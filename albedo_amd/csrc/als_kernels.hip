@@ -1040,15 +1040,38 @@ __global__ __launch_bounds__(Heavy<KP>::NTH, 4) void solve_heavy_kernel(SolveArg
 // Block reductions of the NNLS loop.  Only the NO = KP/64 waves that own coordinates hold nonzero
 // terms, so only they reduce (wave-level DPP/shuffle sums, one partial per wave in LDS); after the
 // barrier every wave reads the NO partials (uniform control flow needs the result everywhere).
+// DPP move of a double (two 32-bit halves); lanes of rows outside ROWMASK, and lanes whose source
+// lies outside the row, read `fill`
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp64(double v, double fill) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(fill), __double2loint(v), CTRL, ROWMASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(fill), __double2hiint(v), CTRL, ROWMASK, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+// Wave-wide fp64 sum / min with the result in lane 63: row_shr 1, 2, 4, 8 within each 16-lane row,
+// then row_bcast:15 and row_bcast:31 across rows (VALU only; a shuffle butterfly is six LDS-latency
+// round trips per value)
+template <bool MIN>
+__device__ __forceinline__ double wave_reduce63(double x) {
+  const double z = MIN ? INFINITY : 0.0;
+  auto op = [](double a, double b) { return MIN ? fmin(a, b) : a + b; };
+  x = op(x, dpp64<0x111, 0xF>(x, z));
+  x = op(x, dpp64<0x112, 0xF>(x, z));
+  x = op(x, dpp64<0x114, 0xF>(x, z));
+  x = op(x, dpp64<0x118, 0xF>(x, z));
+  x = op(x, dpp64<0x142, 0xA>(x, z));
+  x = op(x, dpp64<0x143, 0xC>(x, z));
+  return x;
+}
+
 template <int NO, int N>
 __device__ __forceinline__ void own_sum(double (&v)[N], double* scr, int& phase) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double* sp = scr + phase * 16 * 8;
   if (wave < NO) {
 #pragma unroll
-    for (int n = 0; n < N; ++n)
-      for (int o = 32; o > 0; o >>= 1) v[n] += __shfl_xor(v[n], o);
-    if (lane == 0) {
+    for (int n = 0; n < N; ++n) v[n] = wave_reduce63<false>(v[n]);
+    if (lane == 63) {
 #pragma unroll
       for (int n = 0; n < N; ++n) sp[n * 16 + wave] = v[n];
     }
@@ -1069,8 +1092,8 @@ __device__ __forceinline__ double own_min(double v, double* scr, int& phase) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double* sp = scr + phase * 16 * 8;
   if (wave < NO) {
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
-    if (lane == 0) sp[wave] = v;
+    v = wave_reduce63<true>(v);
+    if (lane == 63) sp[wave] = v;
   }
   __syncthreads();
   v = sp[0];
@@ -1217,7 +1240,7 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
   const bool own = tid < KP;
   const int i = own ? tid : 0;
   const double bi = own ? (double)bvec[i] : 0.0;
-  double xi = 0.0, axi = 0.0, last_dir = 0.0, last_norm = 0.0;
+  double xi = 0.0, axi = 0.0, last_dir = 0.0, last_norm = 0.0, hit = 0.0;
   __syncthreads();
   int phase = 0, last_wall = 0;
   const int iter_max = 400 > 20 * a.kreal ? 400 : 20 * a.kreal;
@@ -1237,8 +1260,9 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
     const double res = own ? axi - bi : 0.0;
     double gi = res;
     if (gi > 0.0 && xi == 0.0) gi = 0.0;
-    double r1[3] = {gi * gi, gi * res, xi * xi};
-    own_sum<NO, 3>(r1, scr, phase);
+    double r1[4] = {gi * gi, gi * res, xi * xi, hit};  // + the previous step's wall hits
+    own_sum<NO, 4>(r1, scr, phase);
+    if (r1[3] > 0.0) last_wall = iterno - 1;
     const double ngrad = r1[0], nx = r1[2];
     const bool cg = iterno > last_wall + 1;
     const double dc = cg ? gi + (ngrad / last_norm) * last_dir : 0.0;
@@ -1270,7 +1294,7 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
     const double cand = (own && step * di > xi) ? xi / di : INFINITY;
     step = fmin(step, own_min<NO>(cand, scr, phase));
     // take the step
-    double hit = 0.0;
+    hit = 0.0;
     if (own) {
       if (step * di > xi * (1 - 1e-14)) {
         xi = 0.0;
@@ -1280,9 +1304,6 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
       }
       axi -= step * adi;
     }
-    double r3[1] = {hit};
-    own_sum<NO, 1>(r3, scr, phase);
-    if (r3[0] > 0.0) last_wall = iterno;
     last_dir = di;
     last_norm = ngrad;
   }
