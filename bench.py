@@ -155,12 +155,18 @@ def main():
     peak = 8000.0
     # HBM bytes of the same kernel from the committed PMC passes of this config (tools/prof.sh ->
     # tools/traffic.py; rocprof cannot run inside the timed bench): GB per sweep, like bytes_per_sweep
+    # The heavy timer covers every kernel of the explicit path: split-K partials + reduce, the wave
+    # kernel, the workgroup kernel (and, with nonnegative, the NNLS kernels)
+    timer_kernels = {"solve_light": ("solve_light",),
+                     "solve_heavy": ("solve_wave", "solve_heavy", "heavy_partial", "heavy_reduce"),
+                     "solve_nnls": ("solve_nnls", "nnls_batch", "heavy_partial", "heavy_reduce")}[dom]
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json")
     if os.path.exists(tpath) and world == 1:
-        entry = json.load(open(tpath)).get(dom)
-        if entry:
-            traffic = entry["hbm_gb_per_sweep"]
+        tj = json.load(open(tpath))
+        found = [tj[n]["hbm_gb_per_sweep"] for n in timer_kernels if n in tj]
+        if found:
+            traffic = float(sum(found))
 
     # ---- top-30 users/s (secondary metric; a bounded user subset) ------------------------------
     topk_ups = None
@@ -195,6 +201,7 @@ def main():
                        "nonnegative": args.config in NONNEGATIVE, "top5_degrees": top_deg},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                          "frac": achieved / peak, "traffic": traffic, "kernel": dom,
+                         "traffic_kernels": list(timer_kernels),
                          "traffic_unit": "GB per sweep (PMC, profiles/pmc_traffic_<config>.json)",
                          "algorithmic_gb_per_sweep": d["bytes_per_sweep"] / 1e9,
                          "kernel_ms_per_sweep": d["ms"]},
