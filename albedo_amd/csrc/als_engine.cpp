@@ -108,6 +108,9 @@ struct Side {
   // split-K of the heavy tail: the first n_split heavy rows (degree > split chunk), their chunks
   int64_t n_split = 0, n_chunks = 0;
   DevBuf d_chunk_row, d_chunk_idx, d_slot0;
+  // nonnegative: the first n_batch rows of the (degree-ascending) light list go to the lockstep
+  // NNLS kernel (degree <= nnls_batch_max_degree)
+  int64_t n_batch = 0, n_batch_nnz = 0;
 };
 
 }  // namespace
@@ -130,6 +133,8 @@ struct als_ctx {
   DevBuf slab, d_G, d_P, d_lam, d_err, d_Gt, d_cs, d_csmax;
   DevBuf d_partial, d_reduced;   // split-K partial / reduced A' records (shared by both sides)
   DevBuf d_iters;                // NNLS iteration counters (sum, max)
+  DevBuf d_gfrag, d_counter;     // lockstep NNLS: G in MFMA operand order, row counter
+  int n_cu = 256;
   int split_len = 0;             // ratings per split-K chunk (0: no split)
   std::vector<float> h_P32, h_lam32, h_Gt;  // host staging of async H2D copies (outlive the sync)
   int slab_blocks = 0;
@@ -220,6 +225,16 @@ int split_chunk_len() {
   return 8192;
 }
 
+// nonnegative = true: rows of degree <= nnls_batch_max_degree run 16 per workgroup in lockstep
+// (nnls_batch.hip) unless ALBEDO_NNLS_BATCH=0 (A/B measurements: every row on solve_nnls_kernel).
+bool use_nnls_batch() {
+  static const bool off = [] {
+    const char* e = std::getenv("ALBEDO_NNLS_BATCH");
+    return e && std::strcmp(e, "0") == 0;
+  }();
+  return !off;
+}
+
 // Heavy rows at padded rank <= 128 run one wave per row (heavy_wave.hip) unless ALBEDO_HEAVY=wg
 // selects the 4-wave workgroup kernel (A/B measurements); rank 256 always uses the workgroup kernel.
 bool use_wave_kernel(const als_ctx* c);
@@ -242,6 +257,18 @@ int rank_layout(als_ctx* c) {
     }
     std::stable_sort(rows[B_HEAVY].begin(), rows[B_HEAVY].end(),
                      [&](int32_t a, int32_t b) { return S.h_deg[a] > S.h_deg[b]; });
+    S.n_batch = S.n_batch_nnz = 0;
+    if (c->p.nonnegative) {  // light rows by ascending degree: the lockstep NNLS kernel's rows first
+      const int64_t dl = use_nnls_batch() ? nnls_batch_max_degree(c->KP) : 0;
+      for (int b = 0; b < B_HEAVY; ++b) {
+        std::stable_sort(rows[b].begin(), rows[b].end(), [&](int32_t x, int32_t y) { return S.h_deg[x] < S.h_deg[y]; });
+        for (int32_t r : rows[b])
+          if (S.h_deg[r] <= dl) {
+            ++S.n_batch;
+            S.n_batch_nnz += S.h_deg[r];
+          }
+      }
+    }
     std::vector<int32_t> all;
     all.reserve(S.own_n);
     for (int b = 0; b < NBUCKET; ++b) {
@@ -491,12 +518,27 @@ int half_sweep_nnls(als_ctx* c, int t) {
   HIPCHK(c->d_iters.ensure(16));
   HIPCHK(hipMemsetAsync(c->d_iters.p, 0, 16, st));
   a.iters = c->d_iters.as<unsigned long long>();
-  TRYC(heavy_launches(c, T, a, 0, T.boff[B_HEAVY], true));
+  const int64_t nb = std::min<int64_t>(T.n_batch, T.boff[B_HEAVY]);
+  if (nb > 0) {
+    HIPCHK(c->d_gfrag.ensure((size_t)KP * KP * 4));
+    HIPCHK(c->d_counter.ensure(64));
+    SolveArgs b = a;
+    b.rows = T.d_rows.as<int32_t>();
+    b.n_rows = nb;
+    // ALBEDO_NNLS_BATCH_WGS caps the persistent grid (tests: force many slot refills per workgroup)
+    const char* ew = std::getenv("ALBEDO_NNLS_BATCH_WGS");
+    const int wgs = (ew && std::atoi(ew) > 0) ? std::min(c->n_cu, std::atoi(ew)) : c->n_cu;
+    HIPCHK(launch_nnls_batch(KP, b, c->d_Gt.as<float>(), c->d_gfrag.as<float>(), c->d_counter.as<unsigned int>(),
+                             wgs, st));
+  }
+  HIPCHK(hipEventRecord(ev[7], st));
+  TRYC(heavy_launches(c, T, a, nb, T.boff[B_HEAVY] - nb, true));
   TRYC(heavy_launches(c, T, a, T.boff[B_HEAVY], T.boff[NBUCKET] - T.boff[B_HEAVY], true));
   a.n_rows = T.boff[NBUCKET];
-  T.stats[0] = T.stats[1] = 0;
-  T.stats[2] = a.n_rows;
-  T.stats[3] = T.own_nnz;
+  T.stats[0] = nb;  // the lockstep kernel's rows and stars, then every other row
+  T.stats[1] = nb > 0 ? T.n_batch_nnz : 0;
+  T.stats[2] = a.n_rows - T.stats[0];
+  T.stats[3] = T.own_nnz - T.stats[1];
   HIPCHK(hipEventRecord(ev[6], st));
   int err = 0;
   unsigned long long it[2] = {0, 0};
@@ -510,9 +552,10 @@ int half_sweep_nnls(als_ctx* c, int t) {
   T.t[ALS_T_EIG] = 0.0;
   T.t[ALS_T_ROTATE] = event_ms(ev[2], ev[3]);
   T.t[ALS_T_COMM] = event_ms(ev[3], ev[4]);
-  T.t[ALS_T_SOLVE_LIGHT] = 0.0;
-  T.t[ALS_T_SOLVE_HEAVY] = event_ms(ev[5], ev[6]);
+  T.t[ALS_T_SOLVE_LIGHT] = event_ms(ev[5], ev[7]);  // lockstep kernel
+  T.t[ALS_T_SOLVE_HEAVY] = event_ms(ev[7], ev[6]);  // per-row kernels (split-K included)
   T.t[ALS_T_HALF_TOTAL] = event_ms(ev[0], ev[6]);
+  if (err & 4) return fail(ALS_E_STATE, "lockstep NNLS row above its degree limit (row layout out of date)");
   if (err) return fail(ALS_E_NOT_POSITIVE_DEFINITE, "NNLS solve produced a non-finite result");
   T.B = S.B;
   T.has_factors = true;
@@ -781,6 +824,7 @@ static int ctx_common(const als_params* p, als_ctx** out) {
     delete c;
     return fail(ALS_E_NO_DEVICE, "device is not gfx950 (MI355X)");
   }
+  c->n_cu = pr.multiProcessorCount;
   if (hipSetDevice(c->dev) != hipSuccess || hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(ALS_E_HIP, "failed to create a HIP stream");

@@ -20,11 +20,23 @@
 #include <cmath>
 #include <cstdint>
 #include <type_traits>
+#include <algorithm>
 #include <utility>
 #include "kernels.h"
 #include "device_common.h"
 
 namespace albedo {
+
+// Workgroup-per-row launches are issued in pieces: an AQL dispatch carries the grid size as a 32-bit
+// count of work-items, so rows x threads must stay below 2^32 (kept at 2^31).
+inline int64_t max_rows_per_launch(int threads) { return (int64_t(1) << 31) / threads; }
+inline SolveArgs chunk_args(const SolveArgs& a, int64_t r0, int threads, int rec_floats) {
+  SolveArgs b = a;
+  b.rows = a.rows + r0;
+  b.n_rows = std::min<int64_t>(a.n_rows - r0, max_rows_per_launch(threads));
+  if (a.prebuilt) b.prebuilt = a.prebuilt + (size_t)r0 * rec_floats;
+  return b;
+}
 
 #ifdef ALBEDO_HEAVY_TIMING  // probes only: per-phase clock64 stamps of the first 64 heavy workgroups
 __device__ unsigned long long albedo_heavy_ts[64][48];
@@ -492,8 +504,16 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
   }
 }
 
-hipError_t launch_solve_light(int KP, int D, const SolveArgs& a, hipStream_t s) {
-  if (a.n_rows <= 0) return hipSuccess;
+hipError_t launch_solve_light(int KP, int D, const SolveArgs& a0, hipStream_t s) {
+  if (a0.n_rows <= 0) return hipSuccess;
+  if (a0.n_rows > max_rows_per_launch(64)) {  // 64 work-items per row: see max_rows_per_launch
+    for (int64_t r0 = 0; r0 < a0.n_rows; r0 += max_rows_per_launch(64)) {
+      const hipError_t e = launch_solve_light(KP, D, chunk_args(a0, r0, 64, 0), s);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  const SolveArgs& a = a0;
   const int blocks = (int)((a.n_rows + 3) / 4);
   const size_t lds = ((size_t)4 * D * (D + 1) + (size_t)4 * KP) * sizeof(float);  // K per wave + D^-1/2
 #define LIGHT(kp, dd) \
@@ -528,12 +548,6 @@ hipError_t launch_solve_light(int KP, int D, const SolveArgs& a, hipStream_t s) 
 constexpr int HT_LD = 17, HT_SZ = 16 * HT_LD;
 __device__ __forceinline__ int htile(int I, int J) { return (I * (I + 1) / 2 + J) * HT_SZ; }
 __device__ __forceinline__ int hel(int r, int c) { return htile(r >> 4, c >> 4) + (r & 15) * HT_LD + (c & 15); }
-// NNLS layout: packed lower 16x16 tiles with 16-float rows (1 KiB per tile, 16-B aligned rows for
-// ds_read_b128), diagonal tiles stored full (both triangles)
-__host__ __device__ __forceinline__ constexpr int ntile(int I, int J) { return (I * (I + 1) / 2 + J) * 256; }
-__host__ __device__ __forceinline__ constexpr int nel(int r, int c) {
-  return ntile(r >> 4, c >> 4) + (r & 15) * 16 + (c & 15);
-}
 
 
 template <int KP>
@@ -1322,9 +1336,16 @@ hipError_t launch_nnls_kp(const SolveArgs& a, const float* Gt, hipStream_t s) {
   static const hipError_t attr2 = allow_lds(solve_nnls_kernel<KP, true>, lds);
   if (attr != hipSuccess) return attr;
   if (attr2 != hipSuccess) return attr2;
-  if (a.prebuilt) solve_nnls_kernel<KP, true><<<(int)a.n_rows, Heavy<KP>::NTH, lds, s>>>(a, Gt);
-  else solve_nnls_kernel<KP, false><<<(int)a.n_rows, Heavy<KP>::NTH, lds, s>>>(a, Gt);
-  return hipGetLastError();
+  // one workgroup per row, in launches of at most 2^31 work-items (an AQL dispatch's grid size is a
+  // 32-bit work-item count: 4.9M rows x 1024 threads would wrap and silently drop rows)
+  for (int64_t r0 = 0; r0 < a.n_rows; r0 += max_rows_per_launch(Heavy<KP>::NTH)) {
+    SolveArgs b = chunk_args(a, r0, Heavy<KP>::NTH, SplitRec<KP>::FLOATS);
+    if (b.prebuilt) solve_nnls_kernel<KP, true><<<(int)b.n_rows, Heavy<KP>::NTH, lds, s>>>(b, Gt);
+    else solve_nnls_kernel<KP, false><<<(int)b.n_rows, Heavy<KP>::NTH, lds, s>>>(b, Gt);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_solve_nnls(int KP, const SolveArgs& a, const float* Gt, hipStream_t s) {
@@ -1344,9 +1365,14 @@ hipError_t launch_heavy_kp(const SolveArgs& a, hipStream_t s) {
   static const hipError_t attr2 = allow_lds(solve_heavy_kernel<KP, 3, true>, lds);
   if (attr != hipSuccess) return attr;
   if (attr2 != hipSuccess) return attr2;
-  if (a.prebuilt) solve_heavy_kernel<KP, 3, true><<<(int)a.n_rows, Heavy<KP>::NTH, lds, s>>>(a);
-  else solve_heavy_kernel<KP><<<(int)a.n_rows, Heavy<KP>::NTH, lds, s>>>(a);
-  return hipGetLastError();
+  for (int64_t r0 = 0; r0 < a.n_rows; r0 += max_rows_per_launch(Heavy<KP>::NTH)) {
+    SolveArgs b = chunk_args(a, r0, Heavy<KP>::NTH, SplitRec<KP>::FLOATS);
+    if (b.prebuilt) solve_heavy_kernel<KP, 3, true><<<(int)b.n_rows, Heavy<KP>::NTH, lds, s>>>(b);
+    else solve_heavy_kernel<KP><<<(int)b.n_rows, Heavy<KP>::NTH, lds, s>>>(b);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_solve_heavy(int KP, const SolveArgs& a, hipStream_t s) {
@@ -1830,11 +1856,11 @@ __global__ __launch_bounds__(256) void topk_rescore_kernel(TopkArgs a) {
 // merged at the end.  P = 1 serves the rows the MFMA pre-selection could not certify; P up to 8
 // serves k up to 512 (recommendForAll* with k > 64, no pre-selection).
 template <int KP, int P>
-__global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32_t* rows) {
+__global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32_t* rows, int64_t row0) {
   __shared__ float msc[4][64 * P];
   __shared__ int mix[4][64 * P];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t si = rows ? rows[blockIdx.x] : (int64_t)blockIdx.x;
+  const int64_t si = rows ? rows[row0 + blockIdx.x] : row0 + (int64_t)blockIdx.x;
   const int srow = a.src_rows[si];
   const float* s = a.S + (int64_t)srow * KP;
   float bs[2 * P];
@@ -1927,8 +1953,13 @@ hipError_t launch_rownorm_max(const float* T, int64_t n, int KP, int kreal, unsi
 
 template <int KP, int P>
 hipError_t topk_exact_p(const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s) {
-  topk_exact_kernel<KP, P><<<(int)n_rows, 256, 0, s>>>(a, rows);
-  return hipGetLastError();
+  for (int64_t r0 = 0; r0 < n_rows; r0 += max_rows_per_launch(256)) {
+    const int64_t n = std::min<int64_t>(n_rows - r0, max_rows_per_launch(256));
+    topk_exact_kernel<KP, P><<<(int)n, 256, 0, s>>>(a, rows, r0);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 template <int KP>
 hipError_t topk_exact_kp(const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s) {

@@ -138,4 +138,11 @@ __device__ __forceinline__ bool chol16(float (&rr)[16], float& dg, int i) {
   return __any(notpd);
 }
 
+// NNLS layout: packed lower 16x16 tiles with 16-float rows (1 KiB per tile, 16-B aligned rows for
+// ds_read_b128), diagonal tiles stored full (both triangles)
+__host__ __device__ __forceinline__ constexpr int ntile(int I, int J) { return (I * (I + 1) / 2 + J) * 256; }
+__host__ __device__ __forceinline__ constexpr int nel(int r, int c) {
+  return ntile(r >> 4, c >> 4) + (r & 15) * 16 + (c & 15);
+}
+
 }  // namespace albedo

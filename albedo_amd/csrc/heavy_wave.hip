@@ -367,6 +367,17 @@ hipError_t launch_wave_kp(const SolveArgs& a, hipStream_t s) {
 
 hipError_t launch_solve_wave(int KP, const SolveArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;
+  constexpr int64_t MAXR = (int64_t(1) << 31) / 64;  // 64 work-items per row; AQL grid sizes are 32-bit
+  if (a.n_rows > MAXR) {
+    for (int64_t r0 = 0; r0 < a.n_rows; r0 += MAXR) {
+      SolveArgs b = a;
+      b.rows = a.rows + r0;
+      b.n_rows = a.n_rows - r0 < MAXR ? a.n_rows - r0 : MAXR;
+      const hipError_t e = launch_solve_wave(KP, b, s);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   if (KP == 64) return launch_wave_kp<64>(a, s);
   if (KP == 128) return launch_wave_kp<128>(a, s);
   return hipErrorInvalidValue;

@@ -64,6 +64,12 @@ hipError_t launch_solve_wave(int KP, const SolveArgs& a, hipStream_t s);
 // nonnegative = true: Spark NNLS per row; Gt = the src Gram in the NNLS tile layout (fp32).
 hipError_t launch_solve_nnls(int KP, const SolveArgs& a, const float* Gt, hipStream_t s);
 int nnls_gtile_floats(int KP);
+// NNLS rows with d <= nnls_batch_max_degree(KP), 16 per workgroup in lockstep (nnls_batch.hip):
+// a persistent grid of at most n_cu workgroups takes rows from *counter (zeroed by the launch);
+// Gfrag: KP*KP floats of scratch for G in MFMA operand order (filled from Gt by the launch)
+int nnls_batch_max_degree(int KP);
+hipError_t launch_nnls_batch(int KP, const SolveArgs& a, const float* Gt, float* Gfrag, unsigned int* counter,
+                             int n_cu, hipStream_t s);
 // colscale[c] = 2^e_c with max_rows |Z[.][c]|·√cmax < 2^13, colscale[KP+c] = 2^-e_c (tmp: KP uints)
 hipError_t launch_colscale(int KP, const float* Z, int64_t n, float cmax, unsigned* tmp, float* colscale,
                            hipStream_t s);

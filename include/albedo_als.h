@@ -149,7 +149,9 @@ enum {
 };
 int als_last_timings(const als_ctx* ctx, int dst_side, double* out, int n);
 /* Rows / nnz handled by each solve path in the last half-sweep of dst_side:
- * out[0]=light rows, out[1]=light nnz, out[2]=heavy rows, out[3]=heavy nnz. */
+ * out[0]=light rows, out[1]=light nnz, out[2]=heavy rows, out[3]=heavy nnz.  With nonnegative =
+ * true "light" is the lockstep NNLS kernel (16 low-degree rows per workgroup) and "heavy" every
+ * other row (one workgroup per row). */
 int als_path_stats(const als_ctx* ctx, int dst_side, int64_t* out4);
 /* NNLS iteration counts of the last half-sweep of dst_side (nonnegative = true):
  * out[0] = iterations summed over rows, out[1] = max over rows, out[2] = rows, out[3] = 0. */

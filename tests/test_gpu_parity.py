@@ -607,3 +607,45 @@ def test_nnls_rank256(gpu_lib):
     _, V = c.factors(1)
     assert np.all(V >= 0)
     assert _rel(V, V_ref) < 1e-3
+
+
+@pytest.mark.parametrize("k,wgs", [(50, 0), (50, 3), (100, 2), (256, 1)])
+def test_nnls_lockstep_light_rows(gpu_lib, monkeypatch, k, wgs):
+    """Low-degree NNLS rows run 16 per workgroup in lockstep (nnls_batch.hip): the user half of a
+    set whose users mostly have 1-6 stars (every lockstep degree limit: 24 / 12 / 6 at KP 64 / 128
+    / 256), row count not a multiple of 16, against the fp64 oracle.  wgs > 0 caps the persistent
+    grid so that every workgroup refills its slots many times.  The path split is checked through
+    als_path_stats (light = lockstep rows)."""
+    from albedo_amd import _lib as L
+    from albedo_amd.synthetic import SynthSpec, generate
+    if wgs:
+        monkeypatch.setenv("ALBEDO_NNLS_BATCH_WGS", str(wgs))
+    n_users = 330 if k == 256 else 613
+    d = generate(SynthSpec(n_users, 90, n_users * 4 + 150, seed=43 + k))
+    B = O.make_blocks(d["user"], d["item"], d["rating"])
+    rng = np.random.default_rng(k)
+    V0 = np.abs(rng.standard_normal((len(B.item_ids), k))).astype(np.float32)
+    V0 /= np.linalg.norm(V0, axis=1, keepdims=True)
+    V0[:, ::3] *= -1.0  # mixed signs: some coordinates end on the wall, others inside
+    p = L.als_params()
+    L.check(gpu_lib.als_params_default(C.byref(p)))
+    p.rank, p.implicit_prefs, p.reg_param, p.alpha, p.nonnegative = k, 1, 0.5, 40.0, 1
+    c = Ctx(gpu_lib, 8)
+    h = C.c_void_p()
+    L.check(gpu_lib.als_create(C.byref(p), C.byref(h)))
+    gpu_lib.als_destroy(c.h)
+    c.h, c.rank = h, k
+    c.ratings(d["user"], d["item"], d["rating"])
+    c.inject(1, B.item_ids, V0)
+    c.inject(0, B.user_ids, np.zeros((len(B.user_ids), k), np.float32))
+    c.half(0)
+    st = np.zeros(4, np.int64)
+    L.check(gpu_lib.als_path_stats(c.h, 0, L.ptr(st, C.c_int64)))
+    dl = {50: 24, 100: 12, 256: 6}[k]
+    deg = np.diff(B.u_ptr)
+    assert st[0] == int(np.sum(deg <= dl)) and st[0] > 250 and st[2] > 0
+    U_ref = O.half_sweep(V0, B.u_ptr, B.u_col, B.u_val, reg=0.5, alpha=40.0, nonnegative=True)
+    _, U = c.factors(0)
+    assert np.all(U >= 0)
+    assert _rel(U, U_ref) < 1e-3
+    assert np.mean((U == 0) == (U_ref == 0)) > 0.995
