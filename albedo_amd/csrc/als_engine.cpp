@@ -109,8 +109,9 @@ struct Side {
   int64_t n_split = 0, n_chunks = 0;
   DevBuf d_chunk_row, d_chunk_idx, d_slot0;
   // nonnegative: the first n_batch rows of the (degree-ascending) light list go to the lockstep
-  // NNLS kernel (degree <= nnls_batch_max_degree)
+  // NNLS kernel, rows [bat_off[v], bat_off[v+1]) with BATCH_SLOTS[v] slots per workgroup
   int64_t n_batch = 0, n_batch_nnz = 0;
+  int64_t bat_off[6] = {0};
 };
 
 }  // namespace
@@ -225,14 +226,22 @@ int split_chunk_len() {
   return 8192;
 }
 
-// nonnegative = true: rows of degree <= nnls_batch_max_degree run 16 per workgroup in lockstep
-// (nnls_batch.hip) unless ALBEDO_NNLS_BATCH=0 (A/B measurements: every row on solve_nnls_kernel).
-bool use_nnls_batch() {
-  static const bool off = [] {
+// nonnegative = true: light rows run in lockstep (nnls_batch.hip), BATCH_SLOTS[v] rows per workgroup
+// for degrees up to nnls_batch_max_degree(KP, slots).  A lockstep iteration costs about the same for
+// any slot count, so the variants pay off down to 8 slots (KP = 256 per row-iteration, tools/probe/
+// batchtime: 16 slots 1.3 us, 8 slots 2.2 us, 4 slots 4.7 us against 4.5 us for solve_nnls_kernel);
+// ALBEDO_NNLS_MINSLOTS=s moves the floor (default 8), ALBEDO_NNLS_BATCH=0 sends every row to
+// solve_nnls_kernel (A/B measurements).
+constexpr int BATCH_SLOTS[5] = {16, 8, 4, 2, 1};
+int64_t nnls_batch_rows_limit(const als_ctx* c, int v) {
+  static const int minslots = [] {
     const char* e = std::getenv("ALBEDO_NNLS_BATCH");
-    return e && std::strcmp(e, "0") == 0;
+    if (e && std::strcmp(e, "0") == 0) return 1 << 20;
+    const char* m = std::getenv("ALBEDO_NNLS_MINSLOTS");
+    return (m && std::atoi(m) > 0) ? std::atoi(m) : 8;
   }();
-  return !off;
+  if (BATCH_SLOTS[v] < minslots) return 0;
+  return std::min<int64_t>(nnls_batch_max_degree(c->KP, BATCH_SLOTS[v]), light_limit(c));
 }
 
 // Heavy rows at padded rank <= 128 run one wave per row (heavy_wave.hip) unless ALBEDO_HEAVY=wg
@@ -258,16 +267,20 @@ int rank_layout(als_ctx* c) {
     std::stable_sort(rows[B_HEAVY].begin(), rows[B_HEAVY].end(),
                      [&](int32_t a, int32_t b) { return S.h_deg[a] > S.h_deg[b]; });
     S.n_batch = S.n_batch_nnz = 0;
+    for (int v = 0; v < 6; ++v) S.bat_off[v] = 0;
     if (c->p.nonnegative) {  // light rows by ascending degree: the lockstep NNLS kernel's rows first
-      const int64_t dl = use_nnls_batch() ? nnls_batch_max_degree(c->KP) : 0;
-      for (int b = 0; b < B_HEAVY; ++b) {
+      for (int b = 0; b < B_HEAVY; ++b)
         std::stable_sort(rows[b].begin(), rows[b].end(), [&](int32_t x, int32_t y) { return S.h_deg[x] < S.h_deg[y]; });
-        for (int32_t r : rows[b])
-          if (S.h_deg[r] <= dl) {
-            ++S.n_batch;
-            S.n_batch_nnz += S.h_deg[r];
-          }
+      // variant v takes the degrees (limit of v-1, limit of v]; the light list is one ascending run
+      int64_t pos = 0;
+      std::vector<int32_t> light;
+      for (int b = 0; b < B_HEAVY; ++b) light.insert(light.end(), rows[b].begin(), rows[b].end());
+      for (int v = 0; v < 5; ++v) {
+        const int64_t dl = nnls_batch_rows_limit(c, v);
+        while (pos < (int64_t)light.size() && S.h_deg[light[pos]] <= dl) S.n_batch_nnz += S.h_deg[light[pos++]];
+        S.bat_off[v + 1] = pos;
       }
+      S.n_batch = pos;
     }
     std::vector<int32_t> all;
     all.reserve(S.own_n);
@@ -477,6 +490,7 @@ int half_sweep_nnls(als_ctx* c, int t) {
   float* zown = S.d_Z.as<float>() + (size_t)c->rank * S.maxrows * KP;
   const int ngt = nnls_gtile_floats(KP);
   std::vector<float> gt(ngt, 0.f);
+  float gscale = 1.0f;
   if (c->p.implicit_prefs) {
     HIPCHK(launch_gram(KP, S.d_X.as<float>(), S.own_n, c->slab.as<double>(), c->slab_blocks, c->d_G.as<double>(), st));
     TRYC(allreduce_G(c));
@@ -489,6 +503,13 @@ int half_sweep_nnls(als_ctx* c, int t) {
     S.GB = S.B;
     for (int i = 0; i < KP; ++i)
       for (int j = 0; j < 16 * ((i >> 4) + 1); ++j) gt[nnls_gtile_index(i, j)] = (float)Gf[(size_t)i * KP + j];
+    double gmax = 0.0;
+    for (double v : Gf) gmax = std::max(gmax, std::fabs(v));
+    if (gmax > 0.0) {  // lockstep kernel's fp16 split of G: max|G|·gscale < 2^15
+      int ex = 0;
+      (void)std::frexp(gmax, &ex);
+      gscale = (float)std::ldexp(1.0, std::max(-120, std::min(120, 15 - ex)));
+    }
   }
   HIPCHK(hipEventRecord(ev[1], st));
   HIPCHK(c->d_Gt.ensure((size_t)ngt * 4));
@@ -515,21 +536,24 @@ int half_sweep_nnls(als_ctx* c, int t) {
   a.reg = (float)c->p.reg_param;
   a.err = c->d_err.as<int>();
   a.colscale = c->d_cs.as<float>();
-  HIPCHK(c->d_iters.ensure(16));
-  HIPCHK(hipMemsetAsync(c->d_iters.p, 0, 16, st));
+  HIPCHK(c->d_iters.ensure(32));  // [sum, max] of every row, then [sum, max] of the lockstep rows
+  HIPCHK(hipMemsetAsync(c->d_iters.p, 0, 32, st));
   a.iters = c->d_iters.as<unsigned long long>();
   const int64_t nb = std::min<int64_t>(T.n_batch, T.boff[B_HEAVY]);
   if (nb > 0) {
     HIPCHK(c->d_gfrag.ensure((size_t)KP * KP * 4));
     HIPCHK(c->d_counter.ensure(64));
-    SolveArgs b = a;
-    b.rows = T.d_rows.as<int32_t>();
-    b.n_rows = nb;
+    HIPCHK(launch_nnls_gfrag(KP, c->d_Gt.as<float>(), gscale, c->d_gfrag.p, st));
     // ALBEDO_NNLS_BATCH_WGS caps the persistent grid (tests: force many slot refills per workgroup)
     const char* ew = std::getenv("ALBEDO_NNLS_BATCH_WGS");
     const int wgs = (ew && std::atoi(ew) > 0) ? std::min(c->n_cu, std::atoi(ew)) : c->n_cu;
-    HIPCHK(launch_nnls_batch(KP, b, c->d_Gt.as<float>(), c->d_gfrag.as<float>(), c->d_counter.as<unsigned int>(),
-                             wgs, st));
+    for (int v = 0; v < 5; ++v) {
+      SolveArgs b = a;
+      b.rows = T.d_rows.as<int32_t>() + T.bat_off[v];
+      b.n_rows = T.bat_off[v + 1] - T.bat_off[v];
+      b.iters = a.iters + 2;
+      HIPCHK(launch_nnls_batch(KP, BATCH_SLOTS[v], b, c->d_gfrag.p, gscale, c->d_counter.as<unsigned int>(), wgs, st));
+    }
   }
   HIPCHK(hipEventRecord(ev[7], st));
   TRYC(heavy_launches(c, T, a, nb, T.boff[B_HEAVY] - nb, true));
@@ -541,13 +565,14 @@ int half_sweep_nnls(als_ctx* c, int t) {
   T.stats[3] = T.own_nnz - T.stats[1];
   HIPCHK(hipEventRecord(ev[6], st));
   int err = 0;
-  unsigned long long it[2] = {0, 0};
+  unsigned long long it[4] = {0, 0, 0, 0};
   HIPCHK(hipMemcpyAsync(&err, c->d_err.p, 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(it, c->d_iters.p, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(it, c->d_iters.p, 32, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  T.solver[0] = (int64_t)it[0];
-  T.solver[1] = (int64_t)it[1];
+  T.solver[0] = (int64_t)(it[0] + it[2]);
+  T.solver[1] = (int64_t)std::max(it[1], it[3]);
   T.solver[2] = T.boff[NBUCKET];
+  T.solver[3] = (int64_t)it[2];
   T.t[ALS_T_GRAM] = event_ms(ev[0], ev[1]);
   T.t[ALS_T_EIG] = 0.0;
   T.t[ALS_T_ROTATE] = event_ms(ev[2], ev[3]);

@@ -45,6 +45,17 @@ __device__ unsigned long long albedo_heavy_ts[64][48];
 #else
 #define HEAVY_TS(k)
 #endif
+#ifdef ALBEDO_NNLS_TIMING  // probes only: NNLS loop phase cycles summed over iterations (thread 0)
+__device__ unsigned long long albedo_nnls_ph[64][8];
+#define NNLS_T0() unsigned long long nt_t = clock64(), nt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define NNLS_PH(k) { const unsigned long long nt_n = clock64(); nt_acc[k] += nt_n - nt_t; nt_t = nt_n; }
+#define NNLS_OUT() \
+  if (threadIdx.x == 0 && blockIdx.x < 64) for (int q = 0; q < 8; ++q) albedo_nnls_ph[blockIdx.x][q] = nt_acc[q]
+#else
+#define NNLS_T0()
+#define NNLS_PH(k)
+#define NNLS_OUT()
+#endif
 
 int padded_rank(int rank) {
   if (rank <= 0) return 0;
@@ -1259,6 +1270,7 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
   int phase = 0, last_wall = 0;
   const int iter_max = 400 > 20 * a.kreal ? 400 : 20 * a.kreal;
   int iterno = 0;
+  NNLS_T0();
   for (; iterno < iter_max; ++iterno) {
     int ot = tid;  // opaque copy of threadIdx.x (see nt_symv)
     asm volatile("" : "+v"(ot));
@@ -1275,7 +1287,9 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
     double gi = res;
     if (gi > 0.0 && xi == 0.0) gi = 0.0;
     double r1[4] = {gi * gi, gi * res, xi * xi, hit};  // + the previous step's wall hits
+    NNLS_PH(0);
     own_sum<NO, 4>(r1, scr, phase);
+    NNLS_PH(1);
     if (r1[3] > 0.0) last_wall = iterno - 1;
     const double ngrad = r1[0], nx = r1[2];
     const bool cg = iterno > last_wall + 1;
@@ -1285,13 +1299,17 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
       v1[i] = (float)dc;
     }
     __syncthreads();
+    NNLS_PH(2);
     if (cg) nt_symv<KP, 2>(smem, vv, yy, wsc, ot);
     else nt_symv<KP, 1>(smem, vv, yy, wsc, ot);
+    NNLS_PH(3);
     __syncthreads();
+    NNLS_PH(4);
     const double agi = own ? (double)y0[i] : 0.0;
     const double adc = (own && cg) ? (double)y1[i] : 0.0;
     double r2[4] = {gi * agi, dc * res, dc * adc, dc * dc};
     own_sum<NO, 4>(r2, scr, phase);
+    NNLS_PH(5);
     double step = r1[1] / (r2[0] + 1e-20);
     double di = gi, adi = agi, ndir = ngrad;
     if (cg) {
@@ -1307,6 +1325,7 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
     // don't run through the walls: step = min(step, x_i / d_i over d_i > 0 with step d_i > x_i)
     const double cand = (own && step * di > xi) ? xi / di : INFINITY;
     step = fmin(step, own_min<NO>(cand, scr, phase));
+    NNLS_PH(6);
     // take the step
     hit = 0.0;
     if (own) {
@@ -1320,7 +1339,9 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
     }
     last_dir = di;
     last_norm = ngrad;
+    NNLS_PH(7);
   }
+  NNLS_OUT();
   if (own) a.X[(int64_t)j * KP + i] = i < a.kreal ? (float)xi : 0.f;
   if (tid == 0 && s_flag[1]) atomicOr(a.err, s_flag[1]);
   if (tid == 0 && a.iters) {

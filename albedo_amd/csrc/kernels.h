@@ -64,12 +64,15 @@ hipError_t launch_solve_wave(int KP, const SolveArgs& a, hipStream_t s);
 // nonnegative = true: Spark NNLS per row; Gt = the src Gram in the NNLS tile layout (fp32).
 hipError_t launch_solve_nnls(int KP, const SolveArgs& a, const float* Gt, hipStream_t s);
 int nnls_gtile_floats(int KP);
-// NNLS rows with d <= nnls_batch_max_degree(KP), 16 per workgroup in lockstep (nnls_batch.hip):
-// a persistent grid of at most n_cu workgroups takes rows from *counter (zeroed by the launch);
-// Gfrag: KP*KP floats of scratch for G in MFMA operand order (filled from Gt by the launch)
-int nnls_batch_max_degree(int KP);
-hipError_t launch_nnls_batch(int KP, const SolveArgs& a, const float* Gt, float* Gfrag, unsigned int* counter,
-                             int n_cu, hipStream_t s);
+// NNLS rows of low degree, `slots` (16/8/4/2/1) per workgroup in lockstep (nnls_batch.hip); a slot
+// holds rows of degree <= nnls_batch_max_degree(KP, slots).  A persistent grid of at most n_cu
+// workgroups takes rows from *counter (zeroed by the launch).  Gfrag: KP*KP*4 bytes holding G·gscale
+// in MFMA operand order as fp16 hi + lo, filled by launch_nnls_gfrag (gscale a power of two with
+// max|G|·gscale < 2^15).
+int nnls_batch_max_degree(int KP, int slots);
+hipError_t launch_nnls_gfrag(int KP, const float* Gt, float gscale, void* Gfrag, hipStream_t s);
+hipError_t launch_nnls_batch(int KP, int slots, const SolveArgs& a, const void* Gfrag, float gscale,
+                             unsigned int* counter, int n_cu, hipStream_t s);
 // colscale[c] = 2^e_c with max_rows |Z[.][c]|·√cmax < 2^13, colscale[KP+c] = 2^-e_c (tmp: KP uints)
 hipError_t launch_colscale(int KP, const float* Z, int64_t n, float cmax, unsigned* tmp, float* colscale,
                            hipStream_t s);

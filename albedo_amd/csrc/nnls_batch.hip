@@ -7,11 +7,17 @@
 // residual follows the steps (A·x_new = A·x - step·A·dir) with an exact refresh every 64 iterations.
 //
 // What changes is how A·v is formed.  A light row's A is the common Gram G plus a rank-d term, so a
-// workgroup keeps G in registers as MFMA A-operand fragments and iterates 16 rows ("slots") at once:
-//   G·[v_0 .. v_15]   one 16-column GEMM on v_mfma_f32_16x16x4_f32 (exact fp32 products, like the
-//                     explicit kernel's fp32 FMAs) -- G is read from registers, never from LDS;
-//   Ỹᵀ(Ỹ v)           per slot, from the slot's Ỹ rows in LDS (d x KP fp32);
+// workgroup iterates up to 16 rows ("slots") at once and never forms A:
+//   G·[v_0 .. v_15]   one 16-column GEMM on v_mfma_f32_16x16x32_f16 with G and every v split into
+//                     fp16 hi + lo (hi·hi + hi·lo + lo·hi, fp32 accumulation: 22-bit operands, as the
+//                     heavy build), G by a power of two, each slot's v by a power of two from a bound
+//                     on max|v| the reductions already carry; G streams from L2 (it is shared by every
+//                     workgroup), v goes through LDS;
+//   Ỹᵀ(Ỹ v)           per slot, fp32, from the slot's Ỹ rows in LDS (d x KP);
 //   λn v              per slot.
+// The Ỹ budget is 96 KiB, so the slot count trades against the degree limit: SV slots of degree
+// <= 24576 / (SV·KP) (KP = 256: 16 x 6, 8 x 12, 4 x 24, 2 x 48, 1 x 96); the G·V cost is the same
+// for any SV (16 MFMA columns), the per-row cost falls as 1/SV.
 // Lane layout = the MFMA C/D layout: wave w owns row blocks I = w·RBW .. w·RBW + RBW-1; lane l holds
 // slot j = l & 15 and coordinates 16 I + 4 (l >> 4) + t, t = 0..3.  Every per-slot vector lives in
 // that layout in registers (fp64, as in the explicit kernel); per-slot sums reduce over the four lane
@@ -23,113 +29,181 @@
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdint>
+#include <utility>
 #include "device_common.h"
 #include "kernels.h"
 
 namespace albedo {
 namespace {
 
-template <int KP>
+constexpr int YBUDGET = 24576;  // floats of Ỹ per workgroup (96 KiB)
+
+#ifdef ALBEDO_BATCH_TIMING  // probes only: loop phase cycles summed over iterations (thread 0)
+__device__ unsigned long long albedo_batch_ph[64][9];
+#define BT_T0() unsigned long long bt_t = clock64(), bt_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}
+#define BT_PH(k) { const unsigned long long bt_n = clock64(); bt_acc[k] += bt_n - bt_t; bt_t = bt_n; }
+#define BT_OUT() \
+  if (threadIdx.x == 0 && blockIdx.x < 64) for (int q = 0; q < 9; ++q) albedo_batch_ph[blockIdx.x][q] = bt_acc[q]
+#else
+#define BT_T0()
+#define BT_PH(k)
+#define BT_OUT()
+#endif
+
+template <int KP, int SV>
 struct NBatch {
   static constexpr int NQ = KP / 16;                 // 16-row blocks of G
+  static constexpr int NS = KP / 32;                 // 32-deep k-steps of the f16 MFMA
   static constexpr int NW = KP >= 128 ? 8 : 4;       // waves
-  static constexpr int RBW = NQ / NW;                // row blocks per wave
+  static constexpr int RBW = NQ / NW;                // row blocks per wave (1 or 2)
   static constexpr int NTH = 64 * NW;
-  static constexpr int S = 16;                       // slots (the MFMA's 16 columns)
-  static constexpr int DL = 1536 / KP;               // max degree: Ỹ of 16 slots = 96 KiB
+  static constexpr int S = 16;                       // MFMA columns; slots SV <= 16 of them
+  static constexpr int DL = YBUDGET / (SV * KP);     // degree limit of a slot
   static constexpr int DLP = (DL + 3) & ~3;
   static constexpr int YS = DL * KP + 4;             // floats per slot; +4: slot j starts on bank 4j
-  static constexpr int RT = 4;                       // refill when this many slots are idle
+  static constexpr int RT = SV >= 4 ? SV / 4 : 1;    // refill when this many slots are idle
   // LDS, in floats
-  static constexpr int OFF_Y = 0;                            // [S][YS]
-  static constexpr int OFF_V = S * YS;                       // [2][NQ][4][16][4]: B fragments
-  static constexpr int OFF_P = OFF_V + 2 * KP * S;           // [2][NW][16][DLP]: Ỹv partials
-  static constexpr int OFF_U = OFF_P + 2 * NW * S * DLP;      // [2][16][DLP]: Ỹv per slot
-  static constexpr int OFF_R = (OFF_U + 2 * S * DLP + 3) & ~3;  // doubles [3][NW][16][4]
-  static constexpr int OFF_C = OFF_R + 2 * 3 * NW * S * 4;      // ints
+  static constexpr int OFF_Y = 0;                            // [SV][YS]
+  static constexpr int OFF_V = SV * YS;                      // [2 vectors][hi|lo][NS][4][16][8] halves
+  static constexpr int OFF_P = OFF_V + 2 * KP * S;           // [2][NW][SV][DLP]: Ỹv partials
+  static constexpr int OFF_U = OFF_P + 2 * NW * SV * DLP;     // [2][SV][DLP]: Ỹv per slot
+  static constexpr int OFF_R = (OFF_U + 2 * SV * DLP + 3) & ~3;  // doubles [2][NW][16][8]
+  static constexpr int OFF_C = OFF_R + 2 * 2 * NW * S * 8;      // ints
   static constexpr int FLOATS = OFF_C + 4;
-  static_assert(NW * RBW == NQ, "row blocks split evenly over the waves");
-  static_assert(FLOATS * 4 <= 160 * 1024, "LDS");
+  static_assert(NW * RBW == NQ && NQ % 2 == 0 && RBW <= 2, "row blocks split evenly over the waves");
+  static_assert(DL >= 1 && FLOATS * 4 <= 160 * 1024, "LDS");
 };
 
 __device__ __forceinline__ bool stop_rule(double step, double ndir, double nx) {
   return isnan(step) || step < 1e-7 || step > 1e40 || ndir < 1e-12 * nx || ndir < 1e-32;
 }
 
-// G in MFMA A-operand order, fp32: Gfrag[((I·NQ + m)·64 + l)·4 + u] = G[16 I + (l & 15)][16 m + 4 u + (l >> 4)]
-// (one 1-KiB coalesced b128 load per wave serves four 16x16x4 steps of row block I)
-__global__ void nnls_gfrag_kernel(const float* __restrict__ Gt, float* __restrict__ Gfrag, int KP) {
-  const int NQ = KP / 16;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= KP * KP) return;
-  const int u = e & 3, l = (e >> 2) & 63, m = (e >> 8) % NQ, I = (e >> 8) / NQ;
-  const int r = 16 * I + (l & 15), c = 16 * m + 4 * u + (l >> 4);
-  Gfrag[e] = (r >> 4) >= (c >> 4) ? Gt[nel(r, c)] : Gt[nel(c, r)];
+// 2^(14 - E) for bound < 2^E: |v| <= bound maps below 2^14, in fp16's range with room for lo
+__device__ __forceinline__ float pow2_scale(double bound) {
+  if (!(bound > 0.0) || !isfinite(bound)) return 1.0f;
+  int e;
+  (void)frexp(bound, &e);
+  e = 14 - e;
+  e = e > 100 ? 100 : (e < -100 ? -100 : e);
+  return ldexpf(1.0f, e);
 }
 
-template <int KP>
-__global__ __launch_bounds__(NBatch<KP>::NTH, 1) void nnls_batch_kernel(SolveArgs a, const float* __restrict__ Gfrag,
-                                                                        unsigned int* __restrict__ counter) {
-  using NB = NBatch<KP>;
-  constexpr int RBW = NB::RBW, NW = NB::NW, DL = NB::DL, DLP = NB::DLP, YS = NB::YS, S = NB::S, NQ = NB::NQ;
+// Sum / max over the four 16-lane rows of the wave (lanes l, l^16, l^32, l^48), every lane getting
+// the same result: v_permlane16_swap pairs rows (0,1) and (2,3), v_permlane32_swap the two halves --
+// VALU only, no LDS round trip (a shuffle is two).  Both partners add in the same order, so the
+// result is bit-identical in all four lanes (the slot state machine relies on that).
+template <bool MAX>
+__device__ __forceinline__ float rows4(float x) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  const float p = __uint_as_float(a[0]), q = __uint_as_float(a[1]);
+  const float s = MAX ? fmaxf(p, q) : p + q;
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  const float u = __uint_as_float(b[0]), v = __uint_as_float(b[1]);
+  return MAX ? fmaxf(u, v) : u + v;
+}
+template <bool MAX>
+__device__ __forceinline__ double rows4(double x) {
+  auto swap16 = [](double d) {
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(d), (unsigned)__double2loint(d), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(d), (unsigned)__double2hiint(d), false, false);
+    return std::make_pair(__hiloint2double((int)hi[0], (int)lo[0]), __hiloint2double((int)hi[1], (int)lo[1]));
+  };
+  auto swap32 = [](double d) {
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(d), (unsigned)__double2loint(d), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(d), (unsigned)__double2hiint(d), false, false);
+    return std::make_pair(__hiloint2double((int)hi[0], (int)lo[0]), __hiloint2double((int)hi[1], (int)lo[1]));
+  };
+  const auto a = swap16(x);
+  const double s = MAX ? fmax(a.first, a.second) : a.first + a.second;
+  const auto b = swap32(s);
+  return MAX ? fmax(b.first, b.second) : b.first + b.second;
+}
+
+// G·gs in MFMA A-operand order, fp16 hi then lo: element ((I·NS + s)·64 + l)·8 + h holds
+// G[16 I + (l & 15)][32 s + 8 (l >> 4) + h] (one 1-KiB b128 load per wave per 32-deep k-step)
+__global__ void nnls_gfrag_kernel(const float* __restrict__ Gt, _Float16* __restrict__ Gh, int KP, float gs) {
+  const int NS = KP / 32;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= KP * KP) return;
+  const int h = e & 7, l = (e >> 3) & 63, s = (e >> 9) % NS, I = (e >> 9) / NS;
+  const int r = 16 * I + (l & 15), c = 32 * s + 8 * (l >> 4) + h;
+  float v = ((r >> 4) >= (c >> 4) ? Gt[nel(r, c)] : Gt[nel(c, r)]) * gs;
+  asm("" : "+v"(v));  // hi and lo from the one fp32 value
+  const _Float16 hi = (_Float16)v;
+  Gh[e] = hi;
+  Gh[KP * KP + e] = (_Float16)(v - (float)hi);
+}
+
+template <int KP, int SV>
+__global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(SolveArgs a, const _Float16* __restrict__ Gh,
+                                                                            float ginv, unsigned int* __restrict__ counter) {
+  using NB = NBatch<KP, SV>;
+  constexpr int RBW = NB::RBW, NW = NB::NW, DL = NB::DL, DLP = NB::DLP, YS = NB::YS, S = NB::S, NS = NB::NS;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int tid = threadIdx.x, lane = tid & 63, j = lane & 15, g = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  float* Yj = smem + NB::OFF_Y + j * YS;  // this lane's slot
+  // Lane coordinates, re-derived every iteration from an opaque copy of threadIdx.x (see the loop
+  // head): otherwise the compiler hoists dozens of LDS addresses out of the loop and spills them.
+  int j = lane & 15, g = lane >> 4;
+  bool slot_lane = j < SV;                          // columns past SV stay empty
+  float* Yj = smem + NB::OFF_Y + (slot_lane ? j : 0) * YS;  // this lane's slot
   double* R = reinterpret_cast<double*>(smem + NB::OFF_R);
   int* ctl = reinterpret_cast<int*>(smem + NB::OFF_C);
+  _Float16* Vh = reinterpret_cast<_Float16*>(smem + NB::OFF_V);
 
-  // this wave's G fragments, streamed from L2 by every product (256 KiB at KP = 256: G is shared by
-  // every workgroup and stays cached; holding it in registers would leave none for the slot state)
-  const float* gwave = Gfrag + ((int64_t)(w * RBW) * NQ * 64 + lane) * 4;
+  // this wave's G fragments (hi; lo follows at + KP·KP halves), streamed from L2 by every product
+  const _Float16* gwave = Gh + ((int64_t)(w * RBW) * NS * 64 + lane) * 8;
 
   auto coord = [&](int rb, int t) { return 16 * (w * RBW + rb) + 4 * g + t; };
+  BT_T0();
 
-  // per-slot sums over the slot's KP coordinates: lane groups by shuffles, waves through LDS
-  auto slot_sum = [&](auto NN, double* v, int red) {
-    constexpr int N = decltype(NN)::value;
+  // Per-slot reductions over the slot's KP coordinates: the four lane groups by shuffles, the waves
+  // through LDS (buffer `buf`, values at `off`..): the first NSUM values are summed, the next NMAX
+  // take the maximum.  Every lane of a slot ends with the same values.
+  auto slot_reduce = [&](auto NSUMC, auto NMAXC, double* v, int buf, int off) {
+    constexpr int NSUM = decltype(NSUMC)::value, N = NSUM + decltype(NMAXC)::value;
 #pragma unroll
-    for (int n = 0; n < N; ++n) {
-      v[n] += __shfl_xor(v[n], 16);
-      v[n] += __shfl_xor(v[n], 32);
-    }
-    double* rp = R + red * NW * S * 4;
+    for (int n = 0; n < N; ++n) v[n] = n < NSUM ? rows4<false>(v[n]) : rows4<true>(v[n]);
+    double* rp = R + buf * NW * S * 8 + off;
     if (g == 0) {
 #pragma unroll
-      for (int n = 0; n < N; ++n) rp[(w * S + j) * 4 + n] = v[n];
+      for (int n = 0; n < N; ++n) rp[(w * S + j) * 8 + n] = v[n];
     }
     __syncthreads();
 #pragma unroll
     for (int n = 0; n < N; ++n) {
-      double t = rp[j * 4 + n];
+      double t = rp[j * 8 + n];
 #pragma unroll
-      for (int u = 1; u < NW; ++u) t += rp[(u * S + j) * 4 + n];
+      for (int u = 1; u < NW; ++u) t = n < NSUM ? t + rp[(u * S + j) * 8 + n] : fmax(t, rp[(u * S + j) * 8 + n]);
       v[n] = t;
     }
   };
-  auto slot_min = [&](double v) {
-    v = fmin(v, __shfl_xor(v, 16));
-    v = fmin(v, __shfl_xor(v, 32));
-    double* rp = R + 2 * NW * S * 4;
-    if (g == 0) rp[(w * S + j) * 4] = v;
-    __syncthreads();
-    double t = rp[j * 4];
-#pragma unroll
-    for (int u = 1; u < NW; ++u) t = fmin(t, rp[(u * S + j) * 4]);
-    return t;
-  };
 
-  // y_n = A·v_n for NV per-slot vectors (fp32 in, fp32 out), lamc = λn (or 1 on pad coordinates)
-  auto product = [&](auto NVV, const float (*vin)[RBW][4], float (*yout)[RBW][4], float lamn) {
+  // y_n = A·v_n for NV per-slot vectors (fp32 in, fp32 out); vs[n]: the slot's power-of-two scale
+  // of v_n for the fp16 split; lamn = λn (1 on pad coordinates)
+  auto product = [&](auto NVV, const float (*vin)[RBW][4], const float* vs, float (*yout)[RBW][4], float lamn) {
     constexpr int NV = decltype(NVV)::value;
-    // B fragments: coordinate 16 m + 4 u + gg of slot j at ((m·4 + gg)·16 + j)·4 + u
+    // B fragments: coordinate 32 s + 8 gg + h of slot j at hi/lo [((s·4 + gg)·16 + j)·8 + h]
 #pragma unroll
     for (int n = 0; n < NV; ++n) {
-      float* V = smem + NB::OFF_V + n * KP * S;
+      _Float16* vh = Vh + n * 2 * KP * S;
+      _Float16* vl = vh + KP * S;
 #pragma unroll
-      for (int rb = 0; rb < RBW; ++rb)
+      for (int rb = 0; rb < RBW; ++rb) {
+        const int I = w * RBW + rb;
+        const int off = (((I >> 1) * 4 + 2 * (I & 1) + (g >> 1)) * 16 + j) * 8 + 4 * (g & 1);
+        f16x4 hv, lv;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) V[(((w * RBW + rb) * 4 + t) * 16 + j) * 4 + g] = vin[n][rb][t];
+        for (int t = 0; t < 4; ++t) {
+          float v = vin[n][rb][t] * vs[n];
+          asm("" : "+v"(v));
+          const _Float16 h = (_Float16)v;
+          hv[t] = h;
+          lv[t] = (_Float16)(v - (float)h);
+        }
+        *reinterpret_cast<f16x4*>(vh + off) = hv;
+        *reinterpret_cast<f16x4*>(vl + off) = lv;
+      }
     }
     // Ỹ v partials over this lane's coordinates (each Ỹ fragment read once for every vector),
     // summed over the four lane groups, one partial per wave and slot
@@ -148,49 +222,56 @@ __global__ __launch_bounds__(NBatch<KP>::NTH, 1) void nnls_batch_kernel(SolveArg
       }
 #pragma unroll
       for (int n = 0; n < NV; ++n) {
-        p[n] += __shfl_xor(p[n], 16);
-        p[n] += __shfl_xor(p[n], 32);
-        if (g == 0) smem[NB::OFF_P + ((n * NW + w) * S + j) * DLP + e] = p[n];
+        p[n] = rows4<false>(p[n]);
+        if (g == 0 && slot_lane) smem[NB::OFF_P + ((n * NW + w) * SV + j) * DLP + e] = p[n];
       }
     }
     __syncthreads();
+    BT_PH(3);
     // per-slot Ỹ v: sum of the partials in a fixed order
-    for (int idx = tid; idx < NV * S * DL; idx += NB::NTH) {
-      const int n = idx / (S * DL), jj = (idx / DL) % S, e = idx % DL;
-      const float* P = smem + NB::OFF_P + n * NW * S * DLP + jj * DLP + e;
+    for (int idx = tid; idx < NV * SV * DL; idx += NB::NTH) {
+      const int n = idx / (SV * DL), jj = (idx / DL) % SV, e = idx % DL;
+      const float* P = smem + NB::OFF_P + n * NW * SV * DLP + jj * DLP + e;
       float t = 0.f;
 #pragma unroll
-      for (int q = 0; q < NW; ++q) t += P[q * S * DLP];
-      smem[NB::OFF_U + (n * S + jj) * DLP + e] = t;
+      for (int q = 0; q < NW; ++q) t += P[q * SV * DLP];
+      smem[NB::OFF_U + (n * SV + jj) * DLP + e] = t;
     }
-    // G·V on MFMA
+    // G·V on split-fp16 MFMA
     f32x4 acc[NV][RBW];
 #pragma unroll
     for (int n = 0; n < NV; ++n)
 #pragma unroll
       for (int rb = 0; rb < RBW; ++rb) acc[n][rb] = zero4();
-    f32x4 gq[RBW], gn[RBW];
-#pragma unroll
-    for (int rb = 0; rb < RBW; ++rb) gq[rb] = ld4(gwave + rb * NQ * 256);
+    // (k-step, row block) pairs in sequence, the next pair's G fragments in flight
+    f16x8 gh = *reinterpret_cast<const f16x8*>(gwave), gl = *reinterpret_cast<const f16x8*>(gwave + KP * KP);
 #pragma unroll 2
-    for (int m = 0; m < NQ; ++m) {
-      if (m + 1 < NQ) {  // next row-block column group in flight while this one is on MFMA
-#pragma unroll
-        for (int rb = 0; rb < RBW; ++rb) gn[rb] = ld4(gwave + rb * NQ * 256 + (m + 1) * 256);
+    for (int q = 0; q < NS * RBW; ++q) {
+      const int ks = q / RBW, rb = q % RBW;
+      f16x8 nh = gh, nl = gl;
+      if (q + 1 < NS * RBW) {
+        const int ks1 = (q + 1) / RBW, rb1 = (q + 1) % RBW;
+        nh = *reinterpret_cast<const f16x8*>(gwave + rb1 * NS * 512 + ks1 * 512);
+        nl = *reinterpret_cast<const f16x8*>(gwave + KP * KP + rb1 * NS * 512 + ks1 * 512);
       }
-      f32x4 vb[NV];
 #pragma unroll
-      for (int n = 0; n < NV; ++n) vb[n] = ld4(smem + NB::OFF_V + n * KP * S + ((m * 4 + g) * 16 + j) * 4);
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int n = 0; n < NV; ++n)
-#pragma unroll
-          for (int rb = 0; rb < RBW; ++rb) acc[n][rb] = mfma4(gq[rb][u], vb[n][u], acc[n][rb]);
-#pragma unroll
-      for (int rb = 0; rb < RBW; ++rb) gq[rb] = gn[rb];
+      for (int n = 0; n < NV; ++n) {
+        const _Float16* vh = Vh + n * 2 * KP * S + ((ks * 4 + g) * 16 + j) * 8;
+        const f16x8 bh = *reinterpret_cast<const f16x8*>(vh);
+        const f16x8 bl = *reinterpret_cast<const f16x8*>(vh + KP * S);
+        f32x4 c = acc[n][0];
+        if (RBW > 1 && rb == 1) c = acc[n][RBW > 1 ? 1 : 0];
+        c = mfma_h(gh, bh, c);
+        c = mfma_h(gh, bl, c);
+        c = mfma_h(gl, bh, c);
+        if (RBW > 1 && rb == 1) acc[n][RBW > 1 ? 1 : 0] = c;
+        else acc[n][0] = c;
+      }
+      gh = nh;
+      gl = nl;
     }
     __syncthreads();
+    BT_PH(4);
     // Ỹᵀ (Ỹ v) + λn v + G v
     float wv[NV][RBW][4];
 #pragma unroll
@@ -199,29 +280,37 @@ __global__ __launch_bounds__(NBatch<KP>::NTH, 1) void nnls_batch_kernel(SolveArg
       for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
         for (int t = 0; t < 4; ++t) wv[n][rb][t] = 0.f;
-#pragma unroll 2
-    for (int e = 0; e < DL; ++e) {
-      float un[NV];
+    // four ratings per step: the slot's Ỹv from one b128 read per vector
+    const float* Uj = smem + NB::OFF_U + (slot_lane ? j : 0) * DLP;
+#pragma unroll 1
+    for (int e4 = 0; e4 < DLP; e4 += 4) {
+      f32x4 u4[NV];
 #pragma unroll
-      for (int n = 0; n < NV; ++n) un[n] = smem[NB::OFF_U + (n * S + j) * DLP + e];
+      for (int n = 0; n < NV; ++n) u4[n] = slot_lane ? ld4(Uj + n * SV * DLP + e4) : zero4();
 #pragma unroll
-      for (int rb = 0; rb < RBW; ++rb) {
-        const f32x4 y4 = ld4(Yj + e * KP + 16 * (w * RBW + rb) + 4 * g);
+      for (int ee = 0; ee < 4; ++ee) {
+        if (DL % 4 != 0 && e4 + ee >= DL) break;
 #pragma unroll
-        for (int n = 0; n < NV; ++n)
+        for (int rb = 0; rb < RBW; ++rb) {
+          const f32x4 y4 = ld4(Yj + (e4 + ee) * KP + 16 * (w * RBW + rb) + 4 * g);
 #pragma unroll
-          for (int t = 0; t < 4; ++t) wv[n][rb][t] = fmaf(y4[t], un[n], wv[n][rb][t]);
+          for (int n = 0; n < NV; ++n)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) wv[n][rb][t] = fmaf(y4[t], u4[n][ee], wv[n][rb][t]);
+        }
       }
     }
 #pragma unroll
-    for (int n = 0; n < NV; ++n)
+    for (int n = 0; n < NV; ++n) {
+      const float unscale = ginv / vs[n];  // powers of two: exact
 #pragma unroll
       for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const float lc = coord(rb, t) < a.kreal ? lamn : 1.0f;
-          yout[n][rb][t] = acc[n][rb][t] + fmaf(lc, vin[n][rb][t], wv[n][rb][t]);
+          yout[n][rb][t] = acc[n][rb][t] * unscale + fmaf(lc, vin[n][rb][t], wv[n][rb][t]);
         }
+    }
   };
 
   // slot state (every lane of a slot holds the slot's scalars)
@@ -229,22 +318,30 @@ __global__ __launch_bounds__(NBatch<KP>::NTH, 1) void nnls_batch_kernel(SolveArg
   float bb[RBW][4];
   bool act = false;
   int row = 0, iterno = 0, last_wall = 0, npos = 0, dd = 0;
-  double last_norm = 0.0, hit = 0.0;
+  double last_norm = 0.0, hit = 0.0, last_dmax = 0.0;
   const int iter_max = 400 > 20 * a.kreal ? 400 : 20 * a.kreal;
   bool exhausted = false;
   int wg_iter = 0;
 
   for (;;) {
+    {
+      int ot = tid;
+      asm volatile("" : "+v"(ot));
+      j = ot & 15;
+      g = (ot >> 4) & 3;
+      slot_lane = j < SV;
+      Yj = smem + NB::OFF_Y + (slot_lane ? j : 0) * YS;
+    }
     // ---- refill idle slots (uniform: every wave sees the same slot flags) ----------------------
-    const unsigned idle = (unsigned)__ballot(lane < 16 && !act) & 0xFFFFu;
+    const unsigned idle = (unsigned)__ballot(slot_lane && !act) & ((1u << SV) - 1u);
     const int nidle = __popc(idle);
-    if (!exhausted && (nidle >= NB::RT || nidle == S)) {
+    if (!exhausted && (nidle >= NB::RT || nidle == SV)) {
       __syncthreads();  // Ỹ of the idle slots is no longer read
       if (tid == 0) ctl[0] = (int)atomicAdd(counter, (unsigned)nidle);
       __syncthreads();
       const int64_t base = ctl[0];
       if (base + nidle >= a.n_rows) exhausted = true;
-      if (!act) {
+      if (slot_lane && !act) {
         const int64_t r = base + __popc(idle & ((1u << j) - 1u));
         if (r < a.n_rows) {
           act = true;
@@ -283,45 +380,57 @@ __global__ __launch_bounds__(NBatch<KP>::NTH, 1) void nnls_batch_kernel(SolveArg
           iterno = 0;
           last_wall = 0;
           last_norm = 0.0;
+          last_dmax = 0.0;
           hit = 0.0;
         }
       }
       __syncthreads();  // the new Ỹ rows before any product reads them
     }
-    if (__ballot(lane < 16 && act) == 0) break;  // drained (implies exhausted)
+    BT_PH(0);
+    if ((__ballot(slot_lane && act) & ((1u << SV) - 1u)) == 0) break;  // drained (implies exhausted)
     const float lamn = a.reg * (float)(a.implicit ? npos : dd);
 
     // ---- exact residual refresh (A·x) every 64 workgroup iterations -----------------------------
     if (wg_iter > 0 && (wg_iter & 63) == 0) {
       float xin[1][RBW][4], yo[1][RBW][4];
+      double xm[1] = {0.0};
 #pragma unroll
       for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) xin[0][rb][t] = (float)x[rb][t];
-      product(std::integral_constant<int, 1>{}, xin, yo, lamn);
+        for (int t = 0; t < 4; ++t) {
+          xin[0][rb][t] = (float)x[rb][t];
+          xm[0] = fmax(xm[0], fabs(x[rb][t]));
+        }
+      slot_reduce(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, xm, 0, 5);
+      const float vs[1] = {pow2_scale(xm[0])};
+      product(std::integral_constant<int, 1>{}, xin, vs, yo, lamn);
 #pragma unroll
       for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
         for (int t = 0; t < 4; ++t) ax[rb][t] = (double)yo[0][rb][t];
     }
     ++wg_iter;
+    BT_PH(1);
 
-    // ---- residual, projected gradient ------------------------------------------------------------
-    double gi[RBW][4];
-    double r1[4] = {0.0, 0.0, 0.0, hit};
+    // ---- residual, projected gradient (recomputed where needed: registers go to the products) ------
+    auto grad = [&](int rb, int t) {
+      const double res = ax[rb][t] - (double)bb[rb][t];
+      return (res > 0.0 && x[rb][t] == 0.0) ? 0.0 : res;
+    };
+    double r1[5] = {0.0, 0.0, 0.0, hit, 0.0};  // Σg², Σg·res, Σx², wall hits | max|g|
 #pragma unroll
     for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const double res = ax[rb][t] - (double)bb[rb][t];
-        double gv = res;
-        if (gv > 0.0 && x[rb][t] == 0.0) gv = 0.0;
-        gi[rb][t] = gv;
+        const double gv = grad(rb, t);
         r1[0] += gv * gv;
         r1[1] += gv * res;
         r1[2] += x[rb][t] * x[rb][t];
+        r1[4] = fmax(r1[4], fabs(gv));
       }
-    slot_sum(std::integral_constant<int, 4>{}, r1, 0);
+    slot_reduce(std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{}, r1, 0, 0);
+    BT_PH(2);
     if (r1[3] > 0.0) last_wall = iterno - 1;
     const double ngrad = r1[0], nx = r1[2];
     const bool cg = iterno > last_wall + 1;
@@ -333,23 +442,36 @@ __global__ __launch_bounds__(NBatch<KP>::NTH, 1) void nnls_batch_kernel(SolveArg
     for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        vin[0][rb][t] = (float)gi[rb][t];
-        vin[1][rb][t] = cg ? (float)(gi[rb][t] + alpha * ld[rb][t]) : 0.f;
+        const double gv = grad(rb, t);
+        vin[0][rb][t] = (float)gv;
+        vin[1][rb][t] = cg ? (float)(gv + alpha * ld[rb][t]) : 0.f;
       }
-    product(std::integral_constant<int, 2>{}, vin, yo, lamn);
-    double r2[4] = {0.0, 0.0, 0.0, 0.0};
+    // max|dir| <= max|g| + |alpha| max|last dir| (one bit of slack at most)
+    const float vs[2] = {pow2_scale(r1[4]), pow2_scale(r1[4] + fabs(alpha) * last_dmax)};
+    product(std::integral_constant<int, 2>{}, vin, vs, yo, lamn);
+    BT_PH(5);
+    // Σg·Ag, Σd·res, Σd·Ad, Σd² | max|d|, and the wall ratios of both candidate directions:
+    // -min x_i/g_i over g_i > 0, -min x_i/d_i over d_i > 0 (Spark clamps the step to the smallest
+    // x_i/dir_i below it; the minimum over every positive dir_i gives the same clamp, so the ratio
+    // rides in this reduction instead of a third one after the direction is chosen)
+    double r2[7] = {0.0, 0.0, 0.0, 0.0, 0.0, -INFINITY, -INFINITY};
 #pragma unroll
     for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const double res = ax[rb][t] - (double)bb[rb][t];
-        const double dc = cg ? gi[rb][t] + alpha * ld[rb][t] : 0.0;
-        r2[0] += gi[rb][t] * (double)yo[0][rb][t];
+        const double gv = grad(rb, t);
+        const double dc = cg ? gv + alpha * ld[rb][t] : 0.0;
+        r2[0] += gv * (double)yo[0][rb][t];
         r2[1] += dc * res;
         r2[2] += dc * (double)yo[1][rb][t];
         r2[3] += dc * dc;
+        r2[4] = fmax(r2[4], fabs(dc));
+        if (gv > 0.0) r2[5] = fmax(r2[5], -(x[rb][t] / gv));
+        if (dc > 0.0) r2[6] = fmax(r2[6], -(x[rb][t] / dc));
       }
-    slot_sum(std::integral_constant<int, 4>{}, r2, 1);
+    slot_reduce(std::integral_constant<int, 4>{}, std::integral_constant<int, 3>{}, r2, 1, 0);
+    BT_PH(6);
     double step = r1[1] / (r2[0] + 1e-20), ndir = ngrad;
     bool use_dc = false;
     if (cg) {
@@ -361,16 +483,9 @@ __global__ __launch_bounds__(NBatch<KP>::NTH, 1) void nnls_batch_kernel(SolveArg
       }
     }
     const bool stop = !act || stop_rule(step, ndir, nx);
-    // don't run through the walls: step = min(step, x_i / d_i over d_i > 0 with step d_i > x_i)
-    double cand = INFINITY;
-#pragma unroll
-    for (int rb = 0; rb < RBW; ++rb)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const double di = use_dc ? gi[rb][t] + alpha * ld[rb][t] : gi[rb][t];
-        if (!stop && step * di > x[rb][t]) cand = fmin(cand, x[rb][t] / di);
-      }
-    step = fmin(step, slot_min(cand));
+    // don't run through the walls
+    step = fmin(step, -(use_dc ? r2[6] : r2[5]));
+    BT_PH(7);
     bool finish = act && stop;
     if (act && !stop) {
       hit = 0.0;
@@ -378,7 +493,8 @@ __global__ __launch_bounds__(NBatch<KP>::NTH, 1) void nnls_batch_kernel(SolveArg
       for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const double di = use_dc ? gi[rb][t] + alpha * ld[rb][t] : gi[rb][t];
+          const double gv = grad(rb, t);
+          const double di = use_dc ? gv + alpha * ld[rb][t] : gv;
           float y0v = yo[0][rb][t], y1v = yo[1][rb][t];
           asm("" : "+v"(y0v), "+v"(y1v));  // a select of values, not of array slots (scratch)
           const double adi = (double)(use_dc ? y1v : y0v);
@@ -392,6 +508,7 @@ __global__ __launch_bounds__(NBatch<KP>::NTH, 1) void nnls_batch_kernel(SolveArg
           ld[rb][t] = di;
         }
       last_norm = ngrad;
+      last_dmax = use_dc ? r2[4] : r1[4];
       ++iterno;
       finish = iterno >= iter_max;
     }
@@ -421,34 +538,57 @@ __global__ __launch_bounds__(NBatch<KP>::NTH, 1) void nnls_batch_kernel(SolveArg
           bb[rb][t] = 0.f;
         }
       hit = 0.0;
+      last_dmax = 0.0;
     }
+    BT_PH(8);
   }
+  BT_OUT();
 }
 
-template <int KP>
-hipError_t launch_batch_kp(const SolveArgs& a, const float* Gfrag, unsigned int* counter, int n_cu, hipStream_t s) {
-  using NB = NBatch<KP>;
-  static const hipError_t attr = allow_lds(nnls_batch_kernel<KP>, NB::FLOATS * 4);
+template <int KP, int SV>
+hipError_t launch_batch_sv(const SolveArgs& a, const _Float16* Gh, float ginv, unsigned int* counter, int n_cu,
+                           hipStream_t s) {
+  using NB = NBatch<KP, SV>;
+  static const hipError_t attr = allow_lds(nnls_batch_kernel<KP, SV>, NB::FLOATS * 4);
   if (attr != hipSuccess) return attr;
   hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned int), s);
   if (e != hipSuccess) return e;
-  const int64_t want = (a.n_rows + NB::S - 1) / NB::S;
+  const int64_t want = (a.n_rows + SV - 1) / SV;
   const int blocks = (int)(want < n_cu ? want : n_cu);
-  nnls_batch_kernel<KP><<<blocks, NB::NTH, NB::FLOATS * 4, s>>>(a, Gfrag, counter);
+  nnls_batch_kernel<KP, SV><<<blocks, NB::NTH, NB::FLOATS * 4, s>>>(a, Gh, ginv, counter);
   return hipGetLastError();
+}
+
+template <int KP>
+hipError_t launch_batch_kp(int sv, const SolveArgs& a, const _Float16* Gh, float ginv, unsigned int* counter,
+                           int n_cu, hipStream_t s) {
+  switch (sv) {
+    case 16: return launch_batch_sv<KP, 16>(a, Gh, ginv, counter, n_cu, s);
+    case 8: return launch_batch_sv<KP, 8>(a, Gh, ginv, counter, n_cu, s);
+    case 4: return launch_batch_sv<KP, 4>(a, Gh, ginv, counter, n_cu, s);
+    case 2: return launch_batch_sv<KP, 2>(a, Gh, ginv, counter, n_cu, s);
+    case 1: return launch_batch_sv<KP, 1>(a, Gh, ginv, counter, n_cu, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 }  // namespace
 
-int nnls_batch_max_degree(int KP) { return KP == 64 ? NBatch<64>::DL : KP == 128 ? NBatch<128>::DL : NBatch<256>::DL; }
+int nnls_batch_max_degree(int KP, int slots) { return (slots >= 1 && slots <= 16) ? YBUDGET / (slots * KP) : 0; }
 
-hipError_t launch_nnls_batch(int KP, const SolveArgs& a, const float* Gt, float* Gfrag, unsigned int* counter,
-                             int n_cu, hipStream_t s) {
+hipError_t launch_nnls_gfrag(int KP, const float* Gt, float gscale, void* Gfrag, hipStream_t s) {
+  nnls_gfrag_kernel<<<(KP * KP + 255) / 256, 256, 0, s>>>(Gt, reinterpret_cast<_Float16*>(Gfrag), KP, gscale);
+  return hipGetLastError();
+}
+
+hipError_t launch_nnls_batch(int KP, int slots, const SolveArgs& a, const void* Gfrag, float gscale,
+                             unsigned int* counter, int n_cu, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;
-  nnls_gfrag_kernel<<<(KP * KP + 255) / 256, 256, 0, s>>>(Gt, Gfrag, KP);
-  if (KP == 64) return launch_batch_kp<64>(a, Gfrag, counter, n_cu, s);
-  if (KP == 128) return launch_batch_kp<128>(a, Gfrag, counter, n_cu, s);
-  if (KP == 256) return launch_batch_kp<256>(a, Gfrag, counter, n_cu, s);
+  const _Float16* Gh = reinterpret_cast<const _Float16*>(Gfrag);
+  const float ginv = 1.0f / gscale;
+  if (KP == 64) return launch_batch_kp<64>(slots, a, Gh, ginv, counter, n_cu, s);
+  if (KP == 128) return launch_batch_kp<128>(slots, a, Gh, ginv, counter, n_cu, s);
+  if (KP == 256) return launch_batch_kp<256>(slots, a, Gh, ginv, counter, n_cu, s);
   return hipErrorInvalidValue;
 }
 

@@ -126,8 +126,11 @@ def main():
         if args.config in NONNEGATIVE:
             sv = np.zeros(4, np.int64)
             L.check(lib.als_solver_stats(h, side, L.ptr(sv, C.c_int64)))
-            nnls_iters["user" if side == 0 else "item"] = {"mean": float(sv[0]) / max(int(sv[2]), 1),
-                                                            "max": int(sv[1]), "rows": int(sv[2])}
+            nb = int(stats[side][0])
+            nnls_iters["user" if side == 0 else "item"] = {
+                "mean": float(sv[0]) / max(int(sv[2]), 1), "max": int(sv[1]), "rows": int(sv[2]),
+                "lockstep_rows": nb, "lockstep_mean": float(sv[3]) / max(nb, 1),
+                "per_row_kernel_mean": float(sv[0] - sv[3]) / max(int(sv[2]) - nb, 1)}
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)

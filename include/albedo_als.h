@@ -154,7 +154,8 @@ int als_last_timings(const als_ctx* ctx, int dst_side, double* out, int n);
  * other row (one workgroup per row). */
 int als_path_stats(const als_ctx* ctx, int dst_side, int64_t* out4);
 /* NNLS iteration counts of the last half-sweep of dst_side (nonnegative = true):
- * out[0] = iterations summed over rows, out[1] = max over rows, out[2] = rows, out[3] = 0. */
+ * out[0] = iterations summed over rows, out[1] = max over rows, out[2] = rows, out[3] = the part of
+ * out[0] spent by the lockstep kernel's rows (als_path_stats out[0]). */
 int als_solver_stats(const als_ctx* ctx, int dst_side, int64_t* out4);
 /* Synchronise the context's streams (bench barrier helper). */
 int als_synchronize(als_ctx* ctx);
