@@ -1112,21 +1112,31 @@ __device__ __forceinline__ void own_sum(double (&v)[N], double* scr, int& phase)
   phase ^= 1;
 }
 
-template <int NO>
-__device__ __forceinline__ double own_min(double v, double* scr, int& phase) {
+// NSUM sums then NMIN minima in one pass (one barrier)
+template <int NO, int NSUM, int NMIN>
+__device__ __forceinline__ void own_sum_min(double (&v)[NSUM + NMIN], double* scr, int& phase) {
+  constexpr int N = NSUM + NMIN;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double* sp = scr + phase * 16 * 8;
   if (wave < NO) {
-    v = wave_reduce63<true>(v);
-    if (lane == 63) sp[wave] = v;
+#pragma unroll
+    for (int n = 0; n < N; ++n) v[n] = n < NSUM ? wave_reduce63<false>(v[n]) : wave_reduce63<true>(v[n]);
+    if (lane == 63) {
+#pragma unroll
+      for (int n = 0; n < N; ++n) sp[n * 16 + wave] = v[n];
+    }
   }
   __syncthreads();
-  v = sp[0];
 #pragma unroll
-  for (int w = 1; w < NO; ++w) v = fmin(v, sp[w]);
+  for (int n = 0; n < N; ++n) {
+    double t = sp[n * 16];
+#pragma unroll
+    for (int w = 1; w < NO; ++w) t = n < NSUM ? t + sp[n * 16 + w] : fmin(t, sp[n * 16 + w]);
+    v[n] = t;
+  }
   phase ^= 1;
-  return v;
 }
+
 
 // y = A·v for NV vectors at once (A symmetric, NNLS layout: packed lower 16x16 tiles, diagonal
 // tiles full; v and y fp32 in LDS).  Wave w takes the row blocks I = w, w + NW, ...; lane l reads
@@ -1307,11 +1317,16 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
     NNLS_PH(4);
     const double agi = own ? (double)y0[i] : 0.0;
     const double adc = (own && cg) ? (double)y1[i] : 0.0;
-    double r2[4] = {gi * agi, dc * res, dc * adc, dc * dc};
-    own_sum<NO, 4>(r2, scr, phase);
+    // + the wall ratios of both candidate directions (min x_i/dir_i over dir_i > 0): clamping the
+    // step to the smallest ratio is Spark's sequential clamp, and riding in this reduction saves the
+    // third one once the direction is chosen
+    double r2[6] = {gi * agi, dc * res, dc * adc, dc * dc, (own && gi > 0.0) ? xi / gi : INFINITY,
+                    (own && dc > 0.0) ? xi / dc : INFINITY};
+    own_sum_min<NO, 4, 2>(r2, scr, phase);
     NNLS_PH(5);
     double step = r1[1] / (r2[0] + 1e-20);
     double di = gi, adi = agi, ndir = ngrad;
+    bool use_dc = false;
     if (cg) {
       const double dstep = r2[1] / (r2[2] + 1e-20);
       if (!nnls_stop(dstep, r2[3], nx)) {  // else: reject the CG direction
@@ -1319,12 +1334,12 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
         di = dc;
         adi = adc;
         ndir = r2[3];
+        use_dc = true;
       }
     }
     if (nnls_stop(step, ndir, nx)) break;
-    // don't run through the walls: step = min(step, x_i / d_i over d_i > 0 with step d_i > x_i)
-    const double cand = (own && step * di > xi) ? xi / di : INFINITY;
-    step = fmin(step, own_min<NO>(cand, scr, phase));
+    // don't run through the walls
+    step = fmin(step, use_dc ? r2[5] : r2[4]);
     NNLS_PH(6);
     // take the step
     hit = 0.0;

@@ -620,6 +620,7 @@ def test_nnls_lockstep_light_rows(gpu_lib, monkeypatch, k, wgs):
     from albedo_amd.synthetic import SynthSpec, generate
     if wgs:
         monkeypatch.setenv("ALBEDO_NNLS_BATCH_WGS", str(wgs))
+    monkeypatch.delenv("ALBEDO_NNLS_MINSLOTS", raising=False)
     n_users = 330 if k == 256 else 613
     d = generate(SynthSpec(n_users, 90, n_users * 4 + 150, seed=43 + k))
     B = O.make_blocks(d["user"], d["item"], d["rating"])
@@ -641,7 +642,9 @@ def test_nnls_lockstep_light_rows(gpu_lib, monkeypatch, k, wgs):
     c.half(0)
     st = np.zeros(4, np.int64)
     L.check(gpu_lib.als_path_stats(c.h, 0, L.ptr(st, C.c_int64)))
-    lim = 32 if k <= 64 else 64  # every light row (degree <= the light limit) runs in lockstep
+    kp = 64 if k <= 64 else (128 if k <= 128 else 256)
+    # light rows (degree <= the light limit) up to the 8-slot variant's limit run in lockstep
+    lim = min(32 if k <= 64 else 64, 24576 // (8 * kp))
     deg = np.diff(B.u_ptr)
     assert st[0] == int(np.sum(deg <= lim)) and st[0] > 250
     if k == 50:
