@@ -84,7 +84,12 @@ struct Side {
   int64_t n = 0;                 // rows (unique raw ids)
   std::vector<int32_t> ids;      // ascending
   std::vector<int64_t> starts;   // shard starts over dense rows (world + 1)
-  int64_t maxrows = 0;           // rows per rank in the padded (gathered) layout
+  int64_t maxrows = 0;           // max own rows over ranks
+  // Gathered (padded) layout, chunk-major so that one chunk of every rank is contiguous: rank r's
+  // local row i sits at (i / chpad)·world·chpad + r·chpad + i % chpad.  world = 1: nch = 1 and
+  // the position is i.  prows() = nch·world·chpad rows.
+  int nch = 1, world = 1;
+  int64_t chpad = 0;
   int64_t own0 = 0, own_n = 0;   // this rank's dense row range
   // dst CSR of this side restricted to own rows (local row index; col = padded src position)
   DevBuf d_ptr, d_col, d_val;
@@ -95,7 +100,11 @@ struct Side {
   int64_t bnnz[NBUCKET] = {0};
   float vmax = 0.f;              // max |rating| over own dst rows (heavy-build fp16 scaling)
   DevBuf d_X;                    // [own_n][KP] factors in basis B
-  DevBuf d_Z;                    // [world*maxrows][KP] rotated factors (src role)
+  DevBuf d_Z;                    // [prows][KP] rotated factors (src role), gathered layout
+  DevBuf d_Xfull;                // world > 1: [prows][KP] every rank's X (basis B), gathered layout
+  bool full_valid = false;       // d_Xfull holds the current X (gathered behind the solve on st2)
+  int64_t prows() const { return (int64_t)nch * world * chpad; }
+  int64_t pos(int r, int64_t i) const { return (i / chpad) * world * chpad + (int64_t)r * chpad + i % chpad; }
   std::vector<double> B;         // [KP][KP] basis: original = X · Bᵀ
   std::vector<double> G;         // last Gram of this side (as src), [rank][rank], in basis GB
   std::vector<double> GB;        // [KP][KP] the side's basis when G was computed (G_orig = GB G GBᵀ)
@@ -112,6 +121,12 @@ struct Side {
   // NNLS kernel, rows [bat_off[v], bat_off[v+1]) with BATCH_SLOTS[v] slots per workgroup
   int64_t n_batch = 0, n_batch_nnz = 0;
   int64_t bat_off[6] = {0};
+  // solve chunks (world > 1, Cholesky path): chunk q's rows of bucket b are the list positions
+  // [cb[b][q], cb[b][q + 1]); its split-K rows are the first split_n[q] of its heavy segment, their
+  // chunk lists start at ck_off[q] and their (chunk-local) slot0 at sl_off[q]
+  int nsolve = 1;
+  int64_t cb[NBUCKET][9] = {{0}};
+  int64_t split_n[8] = {0}, ck_off[9] = {0}, sl_off[8] = {0};
 };
 
 }  // namespace
@@ -140,6 +155,8 @@ struct als_ctx {
   std::vector<float> h_P32, h_lam32, h_Gt;  // host staging of async H2D copies (outlive the sync)
   int slab_blocks = 0;
   hipEvent_t ev[8] = {};
+  hipStream_t st2 = nullptr;     // world > 1: factor-chunk gathers behind the solve
+  hipEvent_t evc[9] = {};        // per solve chunk: done on st; [8]: gathers done on st2
 };
 
 namespace {
@@ -197,20 +214,33 @@ int allreduce_G(als_ctx* c) {
   return ALS_OK;
 }
 
-int allgather_rows(als_ctx* c, float* buf, int64_t rows_per_rank) {
+// in-place all-gather on stream s: rank r's rows_per_rank rows at buf + r·rows_per_rank·KP
+int allgather_rows(als_ctx* c, float* buf, int64_t rows_per_rank, hipStream_t s) {
   if (c->world == 1) return ALS_OK;
   const int64_t per = rows_per_rank * c->KP;
   if (c->comm) {
-    NCCLCHK(ncclAllGather(buf + (int64_t)c->rank * per, buf, per, ncclFloat, c->comm, c->st));
+    NCCLCHK(ncclAllGather(buf + (int64_t)c->rank * per, buf, per, ncclFloat, c->comm, s));
     return ALS_OK;
   }
   std::vector<float> h((size_t)per * c->world);
   HIPCHK(hipMemcpyAsync(h.data() + (size_t)c->rank * per, buf + (int64_t)c->rank * per, per * 4,
-                        hipMemcpyDeviceToHost, c->st));
-  HIPCHK(hipStreamSynchronize(c->st));
+                        hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
   if (c->h_allgather(c->h_user, h.data(), per) != 0) return fail(ALS_E_RCCL, "host all-gather callback failed");
-  HIPCHK(hipMemcpyAsync(buf, h.data(), h.size() * 4, hipMemcpyHostToDevice, c->st));
-  HIPCHK(hipStreamSynchronize(c->st));
+  HIPCHK(hipMemcpyAsync(buf, h.data(), h.size() * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return ALS_OK;
+}
+
+// Gathers layout chunks [q0, q1) of the own rows `own` ([nch·chpad][KP], zero past own_n) into
+// `full` ([prows][KP]) on stream s: chunk q of every rank is one contiguous all-gather.
+int gather_chunks(als_ctx* c, const Side& S, const float* own, float* full, int q0, int q1, hipStream_t s) {
+  const int64_t per = S.chpad * c->KP;
+  for (int q = q0; q < q1; ++q) {
+    float* base = full + (int64_t)q * c->world * per;
+    HIPCHK(hipMemcpyAsync(base + (int64_t)c->rank * per, own + (int64_t)q * per, per * 4, hipMemcpyDeviceToDevice, s));
+    TRYC(allgather_rows(c, base, S.chpad, s));
+  }
   return ALS_OK;
 }
 
@@ -242,6 +272,14 @@ int64_t nnls_batch_rows_limit(const als_ctx* c, int v) {
   }();
   if (BATCH_SLOTS[v] < minslots) return 0;
   return std::min<int64_t>(nnls_batch_max_degree(c->KP, BATCH_SLOTS[v]), light_limit(c));
+}
+
+// world > 1: the solve runs in this many row chunks, each gathered on a second stream while the
+// next one solves; ALBEDO_GATHER_CHUNKS overrides (1..8).
+int gather_chunk_count() {
+  const char* e = std::getenv("ALBEDO_GATHER_CHUNKS");
+  const int n = (e && *e) ? std::atoi(e) : 4;
+  return std::max(1, std::min(8, n));
 }
 
 // Heavy rows at padded rank <= 128 run one wave per row (heavy_wave.hip) unless ALBEDO_HEAVY=wg
@@ -282,29 +320,52 @@ int rank_layout(als_ctx* c) {
       }
       S.n_batch = pos;
     }
+    // world > 1 (Cholesky path): each bucket's rows grouped by solve chunk (= gathered-layout
+    // chunk, local row / chpad), stably, so a chunk's rows of a bucket are one contiguous run
+    const int nsolve = (c->world > 1 && !c->p.nonnegative) ? S.nch : 1;
+    S.nsolve = nsolve;
+    auto chunk_of = [&](int32_t r) { return nsolve == 1 ? 0 : (int)std::min<int64_t>(r / S.chpad, nsolve - 1); };
     std::vector<int32_t> all;
     all.reserve(S.own_n);
     for (int b = 0; b < NBUCKET; ++b) {
       S.boff[b] = (int64_t)all.size();
+      if (nsolve > 1)
+        std::stable_sort(rows[b].begin(), rows[b].end(), [&](int32_t x, int32_t y) { return chunk_of(x) < chunk_of(y); });
+      int64_t p = 0;
+      for (int q = 0; q <= nsolve; ++q) {
+        while (q < nsolve && p < (int64_t)rows[b].size() && chunk_of(rows[b][p]) < q) ++p;
+        S.cb[b][q] = S.boff[b] + (q == nsolve ? (int64_t)rows[b].size() : p);
+      }
       all.insert(all.end(), rows[b].begin(), rows[b].end());
     }
     S.boff[NBUCKET] = (int64_t)all.size();
     HIPCHK(S.d_rows.ensure(all.size() * 4));
     HIPCHK(hipMemcpy(S.d_rows.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
-    // split-K chunks of the heaviest rows (a prefix of the heavy list: sorted by degree)
+    // split-K chunks of each solve chunk's heaviest rows (a prefix of its heavy run: by degree);
+    // slot0 is chunk-local (starts at 0 for every solve chunk)
     const int64_t CH = c->split_len;
-    std::vector<int32_t> crow, cidx, slot0(1, 0);
+    std::vector<int32_t> crow, cidx, slot0;
     S.n_split = 0;
-    for (int32_t r : rows[B_HEAVY]) {
-      if (CH <= 0 || S.h_deg[r] <= CH) break;
-      const int64_t nch = (S.h_deg[r] + CH - 1) / CH;
-      for (int64_t q = 0; q < nch; ++q) {
-        crow.push_back(r);
-        cidx.push_back((int32_t)q);
+    for (int q = 0; q < nsolve; ++q) {
+      S.ck_off[q] = (int64_t)crow.size();
+      S.sl_off[q] = (int64_t)slot0.size();
+      slot0.push_back(0);
+      int64_t n = 0;
+      for (int64_t p = S.cb[B_HEAVY][q]; p < S.cb[B_HEAVY][q + 1]; ++p) {
+        const int32_t r = all[p];
+        if (CH <= 0 || S.h_deg[r] <= CH) break;
+        const int64_t nch = (S.h_deg[r] + CH - 1) / CH;
+        for (int64_t k = 0; k < nch; ++k) {
+          crow.push_back(r);
+          cidx.push_back((int32_t)k);
+        }
+        slot0.push_back((int32_t)((int64_t)crow.size() - S.ck_off[q]));
+        ++n;
       }
-      slot0.push_back((int32_t)crow.size());
-      ++S.n_split;
+      S.split_n[q] = n;
+      S.n_split += n;
     }
+    S.ck_off[nsolve] = (int64_t)crow.size();
     S.n_chunks = (int64_t)crow.size();
     if (S.n_split > 0) {
       HIPCHK(S.d_chunk_row.ensure(crow.size() * 4));
@@ -326,14 +387,21 @@ int rank_layout(als_ctx* c) {
   }
   for (int side = 0; side < 2; ++side) {
     Side& S = c->s[side];
-    HIPCHK(S.d_X.ensure((size_t)std::max<int64_t>(S.own_n, 1) * c->KP * 4));
-    HIPCHK(S.d_Z.ensure((size_t)std::max<int64_t>(c->world * S.maxrows, 1) * c->KP * 4));
+    // X padded to whole layout chunks (zero rows past own_n: they travel in the chunk gathers)
+    HIPCHK(S.d_X.ensure((size_t)std::max<int64_t>(std::max<int64_t>(S.own_n, (int64_t)S.nch * S.chpad), 1) * c->KP * 4));
+    HIPCHK(S.d_Z.ensure((size_t)std::max<int64_t>(S.prows(), 1) * c->KP * 4));
     HIPCHK(hipMemset(S.d_X.p, 0, S.d_X.bytes));
     HIPCHK(hipMemset(S.d_Z.p, 0, S.d_Z.bytes));
+    if (c->world > 1) {
+      HIPCHK(S.d_Xfull.ensure((size_t)std::max<int64_t>(S.prows(), 1) * c->KP * 4));
+      HIPCHK(hipMemset(S.d_Xfull.p, 0, S.d_Xfull.bytes));
+    }
+    S.full_valid = false;
     S.B.assign((size_t)c->KP * c->KP, 0.0);
     for (int i = 0; i < c->KP; ++i) S.B[(size_t)i * c->KP + i] = 1.0;
     S.has_factors = false;
     S.orig_valid = false;
+    S.full_valid = false;
   }
   const int64_t maxsrc = std::max(c->s[0].own_n, c->s[1].own_n);
   c->slab_blocks = gram_slab_blocks(c->KP, maxsrc);
@@ -391,6 +459,9 @@ int ingest_device(als_ctx* c, int64_t n, const int32_t* d_user, const int32_t* d
     for (int r = 0; r < c->world; ++r) S.maxrows = std::max<int64_t>(S.maxrows, S.starts[r + 1] - S.starts[r]);
     S.own0 = S.starts[c->rank];
     S.own_n = S.starts[c->rank + 1] - S.own0;
+    S.world = c->world;
+    S.nch = c->world > 1 ? gather_chunk_count() : 1;
+    S.chpad = std::max<int64_t>(1, (S.maxrows + S.nch - 1) / S.nch);
   }
   ud.release();
   id.release();
@@ -413,7 +484,7 @@ int ingest_device(als_ctx* c, int64_t n, const int32_t* d_user, const int32_t* d
       ShardStarts ss{};
       ss.world = c->world;
       for (int r = 0; r <= c->world; ++r) ss.s[r] = Src.starts[r];
-      HIPCHK(padded_remap(F.col.as<int32_t>() + e0, S.own_nnz, ss, Src.maxrows, S.d_col.as<int32_t>(), st));
+      HIPCHK(padded_remap(F.col.as<int32_t>() + e0, S.own_nnz, ss, Src.chpad, S.d_col.as<int32_t>(), st));
       HIPCHK(hipStreamSynchronize(st));
     }
     S.h_deg.resize(S.own_n);
@@ -443,6 +514,7 @@ int upload_factors(als_ctx* c, int side, const float* f, int64_t ld) {
   for (int i = 0; i < c->KP; ++i) S.B[(size_t)i * c->KP + i] = 1.0;
   S.has_factors = true;
   S.orig_valid = false;
+  S.full_valid = false;
   return ALS_OK;
 }
 
@@ -472,12 +544,12 @@ float event_ms(hipEvent_t a, hipEvent_t b) {
 // fp16 column scales of the heavy build for dst side T over the gathered src rows Z
 int column_scales(als_ctx* c, const Side& S, const Side& T) {
   const float cmax = c->p.implicit_prefs ? (float)c->p.alpha * T.vmax : 1.0f;
-  HIPCHK(launch_colscale(c->KP, S.d_Z.as<float>(), (int64_t)c->world * S.maxrows, cmax, c->d_csmax.as<unsigned>(),
+  HIPCHK(launch_colscale(c->KP, S.d_Z.as<float>(), S.prows(), cmax, c->d_csmax.as<unsigned>(),
                          c->d_cs.as<float>(), c->st));
   return ALS_OK;
 }
 
-int heavy_launches(als_ctx* c, const Side& T, SolveArgs a, int64_t h0, int64_t hn, bool nnls);
+int heavy_launches(als_ctx* c, const Side& T, SolveArgs a, int64_t h0, int64_t hn, bool nnls, int q = 0);
 
 // nonnegative = true: Spark's NNLSSolver in the original basis (no rotation; B stays I)
 int half_sweep_nnls(als_ctx* c, int t) {
@@ -487,7 +559,6 @@ int half_sweep_nnls(als_ctx* c, int t) {
   const int KP = c->KP, k = c->p.rank;
   hipStream_t st = c->st;
   hipEvent_t* ev = c->ev;
-  float* zown = S.d_Z.as<float>() + (size_t)c->rank * S.maxrows * KP;
   const int ngt = nnls_gtile_floats(KP);
   std::vector<float> gt(ngt, 0.f);
   float gscale = 1.0f;
@@ -516,9 +587,9 @@ int half_sweep_nnls(als_ctx* c, int t) {
   HIPCHK(hipMemcpyAsync(c->d_Gt.p, gt.data(), (size_t)ngt * 4, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemsetAsync(c->d_lam.p, 0, KP * 4, st));
   HIPCHK(hipEventRecord(ev[2], st));
-  HIPCHK(hipMemcpyAsync(zown, S.d_X.p, (size_t)S.own_n * KP * 4, hipMemcpyDeviceToDevice, st));
+  if (c->world == 1) HIPCHK(hipMemcpyAsync(S.d_Z.p, S.d_X.p, (size_t)S.own_n * KP * 4, hipMemcpyDeviceToDevice, st));
   HIPCHK(hipEventRecord(ev[3], st));
-  TRYC(allgather_rows(c, S.d_Z.as<float>(), S.maxrows));
+  if (c->world > 1) TRYC(gather_chunks(c, S, S.d_X.as<float>(), S.d_Z.as<float>(), 0, S.nch, st));
   HIPCHK(hipEventRecord(ev[4], st));
   HIPCHK(hipMemsetAsync(c->d_err.p, 0, 4, st));
   TRYC(column_scales(c, S, T));
@@ -585,23 +656,24 @@ int half_sweep_nnls(als_ctx* c, int t) {
   T.B = S.B;
   T.has_factors = true;
   T.orig_valid = false;
+  T.full_valid = false;
   return ALS_OK;
 }
 
-// Heavy launch over rows [h0, h0 + hn) of T's bucket-ordered row list, the first T.n_split of which
-// (when h0 is the heavy bucket's start) are the split-K rows: chunk partials + fp64 reduce, then the
-// factor (or NNLS) from the reduced records, then the remaining rows as usual.
-int heavy_launches(als_ctx* c, const Side& T, SolveArgs a, int64_t h0, int64_t hn, bool nnls) {
+// Heavy launch over rows [h0, h0 + hn) of T's bucket-ordered row list, the first split_n[q] of which
+// (when h0 starts solve chunk q's heavy run) are the split-K rows: chunk partials + fp64 reduce, then
+// the factor (or NNLS) from the reduced records, then the remaining rows as usual.
+int heavy_launches(als_ctx* c, const Side& T, SolveArgs a, int64_t h0, int64_t hn, bool nnls, int q) {
   const int KP = c->KP;
   const int32_t* rows = T.d_rows.as<int32_t>();
-  int64_t ns = (h0 == T.boff[B_HEAVY]) ? std::min<int64_t>(T.n_split, hn) : 0;
+  int64_t ns = (h0 == T.cb[B_HEAVY][q]) ? std::min<int64_t>(T.split_n[q], hn) : 0;
   if (ns > 0) {
     SplitArgs sp{};
-    sp.chunk_row = T.d_chunk_row.as<int32_t>();
-    sp.chunk_idx = T.d_chunk_idx.as<int32_t>();
-    sp.n_chunks = T.n_chunks;
+    sp.chunk_row = T.d_chunk_row.as<int32_t>() + T.ck_off[q];
+    sp.chunk_idx = T.d_chunk_idx.as<int32_t>() + T.ck_off[q];
+    sp.n_chunks = T.ck_off[q + 1] - T.ck_off[q];
     sp.chunk_len = c->split_len;
-    sp.slot0 = T.d_slot0.as<int32_t>();
+    sp.slot0 = T.d_slot0.as<int32_t>() + T.sl_off[q];
     sp.n_split = ns;
     sp.partial = c->d_partial.as<float>();
     sp.reduced = c->d_reduced.as<float>();
@@ -638,11 +710,18 @@ int half_sweep(als_ctx* c, int t) {
   const int KP = c->KP, k = c->p.rank;
   hipStream_t st = c->st;
   hipEvent_t* ev = c->ev;
-  float* zown = S.d_Z.as<float>() + (size_t)c->rank * S.maxrows * KP;
+  const bool multi = c->world > 1;
   double eig_ms = 0.0;
   bool force_heavy = c->p.light_max_degree == 0;
+  // world > 1: the previous half's factor gathers (second stream) finish before any collective or
+  // rotation of this one is issued -- two RCCL operations of one communicator must never overlap
+  if (multi) HIPCHK(hipStreamWaitEvent(st, c->evc[8], 0));
   HIPCHK(hipEventRecord(ev[0], st));
   if (c->p.nonnegative) return half_sweep_nnls(c, t);
+  if (multi && !S.full_valid) {  // src factors set outside a half-sweep (init / injection): gather now
+    TRYC(gather_chunks(c, S, S.d_X.as<float>(), S.d_Xfull.as<float>(), 0, S.nch, st));
+    S.full_valid = true;
+  }
   if (c->p.implicit_prefs) {
     HIPCHK(launch_gram(KP, S.d_X.as<float>(), S.own_n, c->slab.as<double>(), c->slab_blocks, c->d_G.as<double>(), st));
     TRYC(allreduce_G(c));
@@ -694,17 +773,19 @@ int half_sweep(als_ctx* c, int t) {
     HIPCHK(hipMemcpyAsync(c->d_P.p, P32.data(), P32.size() * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(c->d_lam.p, lam32.data(), lam32.size() * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(ev[2], st));
-    HIPCHK(launch_rotate(KP, S.d_X.as<float>(), c->d_P.as<float>(), zown, S.own_n, st));
+    // world > 1: every rank rotates the whole gathered src (no collective on the critical path)
+    if (multi) HIPCHK(launch_rotate(KP, S.d_Xfull.as<float>(), c->d_P.as<float>(), S.d_Z.as<float>(), S.prows(), st));
+    else HIPCHK(launch_rotate(KP, S.d_X.as<float>(), c->d_P.as<float>(), S.d_Z.as<float>(), S.own_n, st));
   } else {
     HIPCHK(hipEventRecord(ev[1], st));
     HIPCHK(hipMemsetAsync(c->d_lam.p, 0, KP * 4, st));
     T.B = S.B;
     if (c->p.reg_param == 0.0) force_heavy = true;
     HIPCHK(hipEventRecord(ev[2], st));
-    HIPCHK(hipMemcpyAsync(zown, S.d_X.p, (size_t)S.own_n * KP * 4, hipMemcpyDeviceToDevice, st));
+    if (multi) HIPCHK(hipMemcpyAsync(S.d_Z.p, S.d_Xfull.p, (size_t)S.prows() * KP * 4, hipMemcpyDeviceToDevice, st));
+    else HIPCHK(hipMemcpyAsync(S.d_Z.p, S.d_X.p, (size_t)S.own_n * KP * 4, hipMemcpyDeviceToDevice, st));
   }
   HIPCHK(hipEventRecord(ev[3], st));
-  TRYC(allgather_rows(c, S.d_Z.as<float>(), S.maxrows));
   TRYC(column_scales(c, S, T));
   HIPCHK(hipEventRecord(ev[4], st));
   HIPCHK(hipMemsetAsync(c->d_err.p, 0, 4, st));
@@ -725,18 +806,34 @@ int half_sweep(als_ctx* c, int t) {
   static const int Dof[3] = {16, 32, 64};
   T.stats[0] = T.stats[1] = T.stats[2] = T.stats[3] = 0;
   for (int b = 0; b < 3; ++b) {
-    a.rows = rows + T.boff[b];
-    a.n_rows = T.boff[b + 1] - T.boff[b];
-    if (force_heavy && use_wave_kernel(c)) HIPCHK(launch_solve_wave(KP, a, st));
-    else if (force_heavy) HIPCHK(launch_solve_heavy(KP, a, st));
-    else HIPCHK(launch_solve_light(KP, Dof[b], a, st));
-    T.stats[force_heavy ? 2 : 0] += a.n_rows;
+    T.stats[force_heavy ? 2 : 0] += T.boff[b + 1] - T.boff[b];
     T.stats[force_heavy ? 3 : 1] += T.bnnz[b];
   }
-  HIPCHK(hipEventRecord(ev[5], st));
-  TRYC(heavy_launches(c, T, a, T.boff[B_HEAVY], T.boff[B_HEAVY + 1] - T.boff[B_HEAVY], false));
   T.stats[2] += T.boff[B_HEAVY + 1] - T.boff[B_HEAVY];
   T.stats[3] += T.bnnz[B_HEAVY];
+  // Solve chunk by chunk (one chunk unless world > 1); world > 1: each finished chunk of the new
+  // factors is gathered on the second stream while the next chunk solves
+  for (int q = 0; q < T.nsolve; ++q) {
+    for (int b = 0; b < 3; ++b) {
+      a.rows = rows + T.cb[b][q];
+      a.n_rows = T.cb[b][q + 1] - T.cb[b][q];
+      if (force_heavy && use_wave_kernel(c)) HIPCHK(launch_solve_wave(KP, a, st));
+      else if (force_heavy) HIPCHK(launch_solve_heavy(KP, a, st));
+      else HIPCHK(launch_solve_light(KP, Dof[b], a, st));
+    }
+    if (T.nsolve == 1) HIPCHK(hipEventRecord(ev[5], st));
+    TRYC(heavy_launches(c, T, a, T.cb[B_HEAVY][q], T.cb[B_HEAVY][q + 1] - T.cb[B_HEAVY][q], false, q));
+    if (multi) {
+      HIPCHK(hipEventRecord(c->evc[q], st));
+      HIPCHK(hipStreamWaitEvent(c->st2, c->evc[q], 0));
+      TRYC(gather_chunks(c, T, T.d_X.as<float>(), T.d_Xfull.as<float>(), q, q + 1, c->st2));
+    }
+  }
+  if (T.nsolve > 1) HIPCHK(hipEventRecord(ev[5], st));  // chunked: the whole solve is timed as heavy
+  if (multi) {
+    if (T.nsolve == 1) TRYC(gather_chunks(c, T, T.d_X.as<float>(), T.d_Xfull.as<float>(), 0, T.nch, c->st2));
+    HIPCHK(hipEventRecord(c->evc[8], c->st2));
+  }
   HIPCHK(hipEventRecord(ev[6], st));
   int err = 0;
   HIPCHK(hipMemcpyAsync(&err, c->d_err.p, 4, hipMemcpyDeviceToHost, st));
@@ -745,8 +842,13 @@ int half_sweep(als_ctx* c, int t) {
   T.t[ALS_T_EIG] = eig_ms;
   T.t[ALS_T_ROTATE] = event_ms(ev[2], ev[3]);
   T.t[ALS_T_COMM] = event_ms(ev[3], ev[4]);
-  T.t[ALS_T_SOLVE_LIGHT] = event_ms(ev[4], ev[5]);
-  T.t[ALS_T_SOLVE_HEAVY] = event_ms(ev[5], ev[6]);
+  if (T.nsolve > 1) {
+    T.t[ALS_T_SOLVE_LIGHT] = 0.0;
+    T.t[ALS_T_SOLVE_HEAVY] = event_ms(ev[4], ev[5]);
+  } else {
+    T.t[ALS_T_SOLVE_LIGHT] = event_ms(ev[4], ev[5]);
+    T.t[ALS_T_SOLVE_HEAVY] = event_ms(ev[5], ev[6]);
+  }
   T.t[ALS_T_HALF_TOTAL] = event_ms(ev[0], ev[6]);
   if (err & 3)
     return fail(ALS_E_NOT_POSITIVE_DEFINITE,
@@ -754,6 +856,7 @@ int half_sweep(als_ctx* c, int t) {
                 "definite. Is A derived from a singular matrix (e.g. collinear column values)?");
   T.has_factors = true;
   T.orig_valid = false;
+  T.full_valid = multi;  // gathered behind the solve (st2); the next half waits for it
   return ALS_OK;
 }
 
@@ -768,19 +871,27 @@ int materialize(als_ctx* c, int side) {
     for (int j = 0; j < KP; ++j) Bt[(size_t)i * KP + j] = (float)S.B[(size_t)j * KP + i];
   HIPCHK(c->d_P.ensure((size_t)KP * KP * 4));
   HIPCHK(hipMemcpyAsync(c->d_P.p, Bt.data(), Bt.size() * 4, hipMemcpyHostToDevice, c->st));
-  DevBuf padded;
-  const int64_t prows = c->world * S.maxrows;
-  HIPCHK(padded.ensure((size_t)std::max<int64_t>(prows, 1) * KP * 4));
-  float* own = padded.as<float>() + (size_t)c->rank * S.maxrows * KP;
-  HIPCHK(launch_rotate(KP, S.d_X.as<float>(), c->d_P.as<float>(), own, S.own_n, c->st));
-  TRYC(allgather_rows(c, padded.as<float>(), S.maxrows));
   HIPCHK(S.d_orig.ensure((size_t)std::max<int64_t>(S.n, 1) * KP * 4));
-  for (int r = 0; r < c->world; ++r) {
-    const int64_t nr = S.starts[r + 1] - S.starts[r];
-    if (nr > 0)
-      HIPCHK(hipMemcpyAsync(S.d_orig.as<float>() + (size_t)S.starts[r] * KP,
-                            padded.as<float>() + (size_t)r * S.maxrows * KP, (size_t)nr * KP * 4,
-                            hipMemcpyDeviceToDevice, c->st));
+  if (c->world == 1) {
+    HIPCHK(launch_rotate(KP, S.d_X.as<float>(), c->d_P.as<float>(), S.d_orig.as<float>(), S.own_n, c->st));
+  } else {  // rotate the own chunks, gather them, unpack the chunk-major layout into dense order
+    if (c->st2) HIPCHK(hipStreamWaitEvent(c->st, c->evc[8], 0));
+    DevBuf own, padded;
+    const int64_t nown = (int64_t)S.nch * S.chpad;
+    HIPCHK(own.ensure((size_t)nown * KP * 4));
+    HIPCHK(padded.ensure((size_t)std::max<int64_t>(S.prows(), 1) * KP * 4));
+    HIPCHK(launch_rotate(KP, S.d_X.as<float>(), c->d_P.as<float>(), own.as<float>(), nown, c->st));
+    TRYC(gather_chunks(c, S, own.as<float>(), padded.as<float>(), 0, S.nch, c->st));
+    for (int r = 0; r < c->world; ++r) {
+      const int64_t nr = S.starts[r + 1] - S.starts[r];
+      for (int q = 0; q < S.nch && (int64_t)q * S.chpad < nr; ++q) {
+        const int64_t l0 = (int64_t)q * S.chpad, cnt = std::min<int64_t>(S.chpad, nr - l0);
+        HIPCHK(hipMemcpyAsync(S.d_orig.as<float>() + (size_t)(S.starts[r] + l0) * KP,
+                              padded.as<float>() + (size_t)S.pos(r, l0) * KP, (size_t)cnt * KP * 4,
+                              hipMemcpyDeviceToDevice, c->st));
+      }
+    }
+    HIPCHK(hipStreamSynchronize(c->st));
   }
   HIPCHK(hipStreamSynchronize(c->st));
   S.orig_valid = true;
@@ -855,6 +966,11 @@ static int ctx_common(const als_params* p, als_ctx** out) {
     return fail(ALS_E_HIP, "failed to create a HIP stream");
   }
   for (auto& e : c->ev) (void)hipEventCreate(&e);
+  for (auto& e : c->evc) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  if (hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return fail(ALS_E_HIP, "failed to create a HIP stream");
+  }
   *out = c;
   return ALS_OK;
 }
@@ -884,8 +1000,12 @@ void als_destroy(als_ctx* c) {
   (void)hipSetDevice(c->dev);
   if (c->st) (void)hipStreamSynchronize(c->st);
   if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->st2) (void)hipStreamSynchronize(c->st2);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->evc)
+    if (e) (void)hipEventDestroy(e);
+  if (c->st2) (void)hipStreamDestroy(c->st2);
   if (c->st) (void)hipStreamDestroy(c->st);
   delete c;
 }
@@ -999,6 +1119,7 @@ int als_init_factors_random(als_ctx* c, uint64_t seed) {
     for (int i = 0; i < c->KP; ++i) S.B[(size_t)i * c->KP + i] = 1.0;
     S.has_factors = true;
     S.orig_valid = false;
+    S.full_valid = false;
   }
   HIPCHK(hipStreamSynchronize(c->st));
   return ALS_OK;
@@ -1112,6 +1233,7 @@ int als_model_create(int32_t rank, int64_t nu, const int32_t* uids, const float*
     S.has_factors = true;
     S.starts = {0, S.n};
     S.maxrows = S.n;
+    S.chpad = std::max<int64_t>(1, S.n);
   }
   *out = c;
   return ALS_OK;
@@ -1283,8 +1405,9 @@ int als_get_row_ratings(als_ctx* c, int side, int32_t id, int64_t cap, int32_t* 
   if (src_ids)
     for (int64_t e = 0; e < n; ++e) {
       const int64_t p = col[e];
-      const int64_t rk = Src.maxrows ? p / Src.maxrows : 0;
-      src_ids[e] = Src.ids[Src.starts[rk] + (p - rk * Src.maxrows)];
+      const int64_t span = (int64_t)Src.world * Src.chpad;  // invert the chunk-major gathered layout
+      const int64_t q = p / span, rem = p % span, rk = rem / Src.chpad;
+      src_ids[e] = Src.ids[Src.starts[rk] + q * Src.chpad + rem % Src.chpad];
     }
   return ALS_OK;
 }

@@ -105,23 +105,24 @@ hipError_t remap_ids(const int32_t* d_ids, int64_t n, int32_t* d_dense, int32_t*
 
 namespace {
 // dense src index -> position in the padded all-gathered layout (rank r's rows at r * maxrows)
-__global__ void padded_remap_kernel(const int32_t* __restrict__ in, int64_t n, ShardStarts st, int64_t maxrows,
+__global__ void padded_remap_kernel(const int32_t* __restrict__ in, int64_t n, ShardStarts st, int64_t chpad,
                                     int32_t* __restrict__ out) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i = in[e];
+    const int64_t d = in[e];
     int r = 0;
-    while (r + 1 < st.world && st.s[r + 1] <= i) ++r;
-    out[e] = (int32_t)(r * maxrows + (i - st.s[r]));
+    while (r + 1 < st.world && st.s[r + 1] <= d) ++r;
+    const int64_t l = d - st.s[r];  // local row of rank r; chunk-major gathered layout
+    out[e] = (int32_t)((l / chpad) * st.world * chpad + r * chpad + l % chpad);
   }
 }
 }  // namespace
 
-hipError_t padded_remap(const int32_t* d_in, int64_t n, const ShardStarts& st, int64_t maxrows, int32_t* d_out,
+hipError_t padded_remap(const int32_t* d_in, int64_t n, const ShardStarts& st, int64_t chpad, int32_t* d_out,
                         hipStream_t s) {
   if (n <= 0) return hipSuccess;
   int64_t blocks = (n + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  padded_remap_kernel<<<(int)blocks, 256, 0, s>>>(d_in, n, st, maxrows, d_out);
+  padded_remap_kernel<<<(int)blocks, 256, 0, s>>>(d_in, n, st, chpad, d_out);
   return hipGetLastError();
 }
 

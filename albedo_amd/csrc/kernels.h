@@ -129,8 +129,9 @@ struct ShardStarts {
   int64_t s[17];
   int world;
 };
-// out[e] = padded all-gather position of dense src row in[e] (rank r's rows start at r * maxrows)
-hipError_t padded_remap(const int32_t* d_in, int64_t n, const ShardStarts& st, int64_t maxrows, int32_t* d_out,
+// out[e] = gathered-layout position of dense src row in[e]: local row l of rank r at
+// (l / chpad)·world·chpad + r·chpad + l % chpad (chunk-major: one chunk of every rank is contiguous)
+hipError_t padded_remap(const int32_t* d_in, int64_t n, const ShardStarts& st, int64_t chpad, int32_t* d_out,
                         hipStream_t s);
 // Synthetic generator (synth.hip)
 hipError_t synth_fill(uint64_t seed, int rounds, int64_t n_users, int64_t n_items,

@@ -32,7 +32,7 @@ def main():
     rng = np.random.default_rng(3)
     U0 = rng.standard_normal((len(B.user_ids), k)).astype(np.float32)
     V0 = rng.standard_normal((len(B.item_ids), k)).astype(np.float32)
-    if mode == "gpu":
+    if mode in ("gpu", "gpunn"):
         def allreduce(_u, buf, n):
             t = torch.from_numpy(np.ctypeslib.as_array(buf, shape=(n,)))
             dist.all_reduce(t)
@@ -50,6 +50,7 @@ def main():
         p = L.als_params()
         L.check(lib.als_params_default(C.byref(p)))
         p.rank, p.implicit_prefs, p.reg_param, p.alpha, p.max_iter = k, 1, 0.5, 40.0, 3
+        p.nonnegative = 1 if mode == "gpunn" else 0
         h = C.c_void_p()
         L.check(lib.als_create(C.byref(p), C.byref(h)))
         L.check(lib.als_comm_init_host(h, rank, world, ar, ag, None))

@@ -62,12 +62,14 @@ def test_sharded_layout_cpu(tmp_path, world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_fit_gpu_matches_single(gpu_lib, tmp_path, world):
-    """Ranks sharing the box's GPU run the engine's sharded fit (device padded remap, host
-    transport for the Gram all-reduce and the factor all-gather); factors match one rank."""
-    res = _launch("gpu", str(tmp_path / "gpu.npz"), world=world)
+@pytest.mark.parametrize("world,nonneg", [(2, False), (3, False), (3, True)])
+def test_sharded_fit_gpu_matches_single(gpu_lib, tmp_path, world, nonneg):
+    """Ranks sharing the box's GPU run the engine's sharded fit (device remap into the chunk-major
+    gathered layout, the solve in row chunks whose factors are gathered on a second stream, host
+    transport for the Gram all-reduce and the all-gathers); factors match the single-process oracle.
+    nonneg: the NNLS half-sweeps (lockstep + per-row kernels) with the blocking chunk gathers."""
+    res = _launch("gpunn" if nonneg else "gpu", str(tmp_path / "gpu.npz"), world=world)
     B, U0, V0 = _problem()
-    U, V = O.fit(B, rank=16, max_iter=3, reg=0.5, alpha=40.0, init_user=U0, init_item=V0)
+    U, V = O.fit(B, rank=16, max_iter=3, reg=0.5, alpha=40.0, init_user=U0, init_item=V0, nonnegative=nonneg)
     rel = lambda a, b: np.max(np.abs(a - b)) / np.max(np.abs(b))
     assert rel(res["U"], U) < 1e-3 and rel(res["V"], V) < 1e-3
