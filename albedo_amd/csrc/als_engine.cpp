@@ -151,6 +151,9 @@ struct als_ctx {
   DevBuf d_iters;                // NNLS iteration counters (sum, max)
   DevBuf d_gfrag, d_counter;     // lockstep NNLS: G in MFMA operand order, row counter
   int n_cu = 256;
+  // top-k counters, cumulative: [0] rows through the MFMA scan, [1] rows re-scored by the exact scan
+  // (certification misses), [2] dst chunks scanned, [3] dst chunks a full scan would take
+  int64_t topk_stats[4] = {0, 0, 0, 0};
   int split_len = 0;             // ratings per split-K chunk (0: no split)
   std::vector<float> h_P32, h_lam32, h_Gt;  // host staging of async H2D copies (outlive the sync)
   int slab_blocks = 0;
@@ -1284,7 +1287,7 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
     tmax = nr[0];
     smax = nr[1];
   }
-  // |entry| <= row norm, so scaling by 2^(13 - ceil(log2 max norm)) keeps every split value < 2^13
+  // |entry| <= row norm, so scaling by 2^(13 - ceil(log2 max norm)) keeps every fp16 value < 2^13
   auto pow2_scale = [](double m) {
     if (!(m > 0.0) || !std::isfinite(m)) return 1.0;
     int e = 0;
@@ -1293,24 +1296,39 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
     return std::ldexp(1.0, e);
   };
   const double ssc = pow2_scale(smax), tsc = pow2_scale(tmax);
-  DevBuf d_tsplit;
-  HIPCHK(d_tsplit.ensure((size_t)T.n * KP * 4));
-  HIPCHK(launch_split_rows(T.d_orig.as<float>(), T.n, KP, (float)tsc, d_tsplit.p, c->st));
-  DevBuf d_dstids;
+  // dst side in descending-norm order, fp16 rows + chunk head norms (topk.hip)
+  const int CH = topk_chunk_rows(KP);
+  const int64_t n_chunks = (T.n + CH - 1) / CH;
+  DevBuf d_th, d_head, d_keys, d_perm, d_tmp, d_dstids;
+  if (!exact_only) {
+    HIPCHK(d_th.ensure((size_t)n_chunks * CH * KP * 2));
+    HIPCHK(d_head.ensure((size_t)n_chunks * 4));
+    HIPCHK(d_keys.ensure((size_t)T.n * 8));
+    HIPCHK(d_perm.ensure((size_t)T.n * 8));
+    const size_t tb = topk_sort_temp_bytes(T.n);
+    HIPCHK(d_tmp.ensure(std::max<size_t>(tb, 16)));
+    HIPCHK(topk_prepare(KP, c->p.rank, T.d_orig.as<float>(), T.n, (float)tsc, d_tmp.p, tb, d_keys.as<uint32_t>(),
+                        d_perm.as<uint32_t>(), d_th.p, d_head.as<float>(), c->st));
+  }
   HIPCHK(d_dstids.ensure(T.n * 4));
-  HIPCHK(hipMemcpy(d_dstids.p, T.ids.data(), T.n * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpyAsync(d_dstids.p, T.ids.data(), T.n * 4, hipMemcpyHostToDevice, c->st));
   const int64_t chunk = 1 << 20;
-  DevBuf d_src, d_cand, d_cs, d_oid, d_osc, d_need, d_flag;
+  DevBuf d_src, d_ls, d_li, d_lc, d_oid, d_osc, d_need, d_flag, d_scan;
+  HIPCHK(d_scan.ensure(8));
   for (int64_t q0 = 0; q0 < (int64_t)known.size(); q0 += chunk) {
     const int64_t nc = std::min<int64_t>(chunk, (int64_t)known.size() - q0);
     HIPCHK(d_src.ensure(nc * 4));
-    HIPCHK(d_cand.ensure(nc * TOPK_KC * 4));
-    HIPCHK(d_cs.ensure(nc * TOPK_KC * 4));
     HIPCHK(d_oid.ensure(nc * k * 4));
     HIPCHK(d_osc.ensure(nc * k * 4));
     HIPCHK(d_need.ensure(nc * 4));
-    HIPCHK(hipMemcpy(d_src.p, known.data() + q0, nc * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemset(d_need.p, 0, nc * 4));
+    if (!exact_only) {
+      HIPCHK(d_ls.ensure(nc * TOPK_CAP * 4));
+      HIPCHK(d_li.ensure(nc * TOPK_CAP * 4));
+      HIPCHK(d_lc.ensure(nc * 4));
+    }
+    HIPCHK(hipMemcpyAsync(d_src.p, known.data() + q0, nc * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemsetAsync(d_need.p, 0, nc * 4, c->st));
+    HIPCHK(hipMemsetAsync(d_scan.p, 0, 8, c->st));
     TopkArgs a{};
     a.S = S.d_orig.as<float>();
     a.T = T.d_orig.as<float>();
@@ -1321,24 +1339,37 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
     a.kreal = c->p.rank;
     a.k = k;
     a.tmax_norm = (float)(tmax * (1.0 + 1e-6));
-    a.Tsplit = d_tsplit.p;
+    a.Th = d_th.p;
+    a.head = d_head.as<float>();
+    a.perm = d_perm.as<uint32_t>();
+    a.n_chunks = n_chunks;
     a.ssc = (float)ssc;
+    a.tsc = (float)tsc;
     a.unscale = (float)(1.0 / (ssc * tsc));
-    a.cand = d_cand.as<int32_t>();
-    a.cand_score = d_cs.as<float>();
+    a.scaled = (float)(ssc * tsc);
+    a.lscore = d_ls.as<float>();
+    a.lidx = d_li.as<int32_t>();
+    a.lcnt = d_lc.as<int32_t>();
     a.out_ids = d_oid.as<int32_t>();
     a.out_scores = d_osc.as<float>();
     a.need_exact = d_need.as<int32_t>();
+    a.scanned = d_scan.as<unsigned long long>();
     if (exact_only) {
       HIPCHK(launch_topk_exact(KP, a, nullptr, nc, c->st));
     } else {
-      HIPCHK(launch_topk(KP, a, c->st));
+      HIPCHK(launch_topk(KP, a, c->n_cu, c->st));
       std::vector<int32_t> need(nc);
       HIPCHK(hipMemcpyAsync(need.data(), d_need.p, nc * 4, hipMemcpyDeviceToHost, c->st));
       HIPCHK(hipStreamSynchronize(c->st));
       std::vector<int32_t> flagged;
       for (int64_t i = 0; i < nc; ++i)
         if (need[i]) flagged.push_back((int32_t)i);
+      unsigned long long scanned = 0;
+      HIPCHK(hipMemcpy(&scanned, d_scan.p, 8, hipMemcpyDeviceToHost));
+      c->topk_stats[0] += nc;
+      c->topk_stats[1] += (int64_t)flagged.size();
+      c->topk_stats[2] += (int64_t)scanned;
+      c->topk_stats[3] += (nc + topk_rows_per_workgroup(KP, nc, c->n_cu) - 1) / topk_rows_per_workgroup(KP, nc, c->n_cu) * n_chunks;
       if (!flagged.empty()) {
         HIPCHK(d_flag.ensure(flagged.size() * 4));
         HIPCHK(hipMemcpy(d_flag.p, flagged.data(), flagged.size() * 4, hipMemcpyHostToDevice));
@@ -1436,6 +1467,12 @@ int als_path_stats(const als_ctx* c, int dst_side, int64_t* out4) {
 int als_solver_stats(const als_ctx* c, int dst_side, int64_t* out4) {
   if (!c || (dst_side != 0 && dst_side != 1) || !out4) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
   for (int i = 0; i < 4; ++i) out4[i] = c->s[dst_side].solver[i];
+  return ALS_OK;
+}
+
+int als_topk_stats(const als_ctx* c, int64_t* out4) {
+  if (!c || !out4) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  for (int i = 0; i < 4; ++i) out4[i] = c->topk_stats[i];
   return ALS_OK;
 }
 

@@ -29,7 +29,6 @@ namespace albedo {
 
 // Workgroup-per-row launches are issued in pieces: an AQL dispatch carries the grid size as a 32-bit
 // count of work-items, so rows x threads must stay below 2^32 (kept at 2^31).
-inline int64_t max_rows_per_launch(int threads) { return (int64_t(1) << 31) / threads; }
 inline SolveArgs chunk_args(const SolveArgs& a, int64_t r0, int threads, int rec_floats) {
   SolveArgs b = a;
   b.rows = a.rows + r0;
@@ -1552,15 +1551,6 @@ hipError_t launch_init_random(int KP, int kreal, float* X, int64_t n, uint64_t s
 // =============================================================================================
 // ALSModel.transform: F2J sdot (netlib sdot.f via F2J: float products added left to right, no FMA)
 // =============================================================================================
-__device__ __forceinline__ float f2j_dot(const float* __restrict__ x, const float* __restrict__ y, int k) {
-#pragma clang fp contract(off)
-  float acc = 0.f;
-  for (int c = 0; c < k; ++c) {
-    const float p = x[c] * y[c];
-    acc = acc + p;
-  }
-  return acc;
-}
 
 __global__ void predict_kernel(int KP, int kreal, const float* __restrict__ U, const float* __restrict__ V,
                                const int32_t* __restrict__ u, const int32_t* __restrict__ v,
@@ -1577,440 +1567,6 @@ hipError_t launch_predict(int KP, int kreal, const float* U, const float* V, con
   if (n <= 0) return hipSuccess;
   predict_kernel<<<(int)((n + 255) / 256), 256, 0, s>>>(KP, kreal, U, V, u, v, out, n);
   return hipGetLastError();
-}
-
-// =============================================================================================
-// Top-k (ALSRecommender.recommendForUsers / ALSModel.recommendForAll):
-//  pass 1  MFMA fp32 scores of 16 src rows x a stripe of dst rows per wave, candidates above a
-//          per-row threshold appended to LDS lists, lists compacted (bitonic) to the best KC;
-//          the 4 waves' lists are merged and the best KC written out;
-//  pass 2  exact F2J rescoring of the KC candidates, sort (score desc, id asc), certification:
-//          any non-candidate has approx <= t (the KC-th approx score) so exact <= t + e; if the
-//          k-th exact score is not > t + e the row is flagged for an exact full scan.
-// =============================================================================================
-
-// key order: higher score first, then lower index
-__device__ __forceinline__ bool tk_before(float s1, int i1, float s2, int i2) {
-  return s1 > s2 || (s1 == s2 && (unsigned)i1 < (unsigned)i2);
-}
-
-// Sort 64*NPL (score, idx) pairs held NPL per lane (element e = lane + 64*h) into tk order
-// (best first).  Fully unrolled so every register index is a compile-time constant.
-template <int NPL, int K, int JJ>
-__device__ __forceinline__ void bitonic_step(float (&sc)[NPL], int (&ix)[NPL], int lane) {
-  if constexpr (JJ >= 64) {
-    constexpr int hj = JJ >> 6;
-    static_for<0, NPL>([&](auto hc) {
-      constexpr int h = decltype(hc)::value, hp = h ^ hj;
-      if constexpr (hp > h) {
-        const int e = lane + 64 * h;
-        const bool up = (e & K) == 0;
-        const bool sw = up ? tk_before(sc[hp], ix[hp], sc[h], ix[h]) : tk_before(sc[h], ix[h], sc[hp], ix[hp]);
-        if (sw) { const float ts = sc[h]; sc[h] = sc[hp]; sc[hp] = ts; const int ti = ix[h]; ix[h] = ix[hp]; ix[hp] = ti; }
-      }
-    });
-  } else {
-    static_for<0, NPL>([&](auto hc) {
-      constexpr int h = decltype(hc)::value;
-      const float os = __shfl_xor(sc[h], JJ);
-      const int oi = __shfl_xor(ix[h], JJ);
-      const int e = lane + 64 * h;
-      const bool lower = (lane & JJ) == 0;
-      const bool up = (e & K) == 0;
-      const bool other_first = tk_before(os, oi, sc[h], ix[h]);
-      const bool take = (lower == up) ? other_first : !other_first;
-      if (take) { sc[h] = os; ix[h] = oi; }
-    });
-  }
-}
-template <int NPL, int K, int JJ>
-__device__ __forceinline__ void bitonic_merge(float (&sc)[NPL], int (&ix)[NPL], int lane) {
-  if constexpr (JJ > 0) {
-    bitonic_step<NPL, K, JJ>(sc, ix, lane);
-    bitonic_merge<NPL, K, JJ / 2>(sc, ix, lane);
-  }
-}
-template <int NPL, int K>
-__device__ __forceinline__ void bitonic_stages(float (&sc)[NPL], int (&ix)[NPL], int lane) {
-  if constexpr (K <= 64 * NPL) {
-    bitonic_merge<NPL, K, K / 2>(sc, ix, lane);
-    bitonic_stages<NPL, 2 * K>(sc, ix, lane);
-  }
-}
-template <int NPL>
-__device__ __forceinline__ void wave_bitonic(float (&sc)[NPL], int (&ix)[NPL]) {
-  bitonic_stages<NPL, 2>(sc, ix, threadIdx.x & 63);
-}
-
-// Pass 1: one workgroup per 64 src rows (wave w owns rows 16w .. 16w+15); scores on split-fp16
-// MFMA: every factor row is scaled by a power of two (max |v| < 2^13) and split into fp16 hi + lo,
-// and hi·hi + hi·lo + lo·hi is accumulated with v_mfma_f32_16x16x32_f16 — products to 2^-22, the
-// same order as fp32 rounding, at 16/3 the fp32-MFMA rate.  The pre-selection only has to keep a
-// superset of the top k: the rescoring pass certifies it with a bound that includes this error.
-// The src fragments live in registers (hi/lo f16x8 per 32 columns); the dst rows (pre-split by
-// split_rows) stream through LDS in chunks of NI, the next chunk prefetched into registers while
-// the current one is on MFMA, rows stored with their 16-B units XOR-swizzled by 4·(row&3) so a
-// fragment read (16 rows x 4 consecutive units) spreads over the banks.  Every workgroup walks
-// the dst rows in the same order, so an XCD's workgroups share the chunks in L2.
-// Candidate lists hold CAP entries per src row and are compacted to the best 64 (threshold = the
-// 64th) only when fewer than 64 slots remain: arrivals decay like 64/n over the scan.
-template <int KP>
-struct TopkLds {
-  static constexpr int NI = 8192 / KP, NJ = NI / 16;           // dst rows per 32 KB LDS chunk
-  static constexpr int RB = 4 * KP;                               // bytes per split dst row
-  static constexpr int CAP = 88;                                  // list capacity per src row
-  static constexpr int NSORT = 2;                                 // sort width per lane (128 slots)
-  static constexpr int CHUNK = NI * KP;                           // floats (NI * RB bytes)
-  static constexpr int LISTS = 64 * CAP;                          // (score, idx) per src row
-  static constexpr int FLOATS = CHUNK + 2 * LISTS + 128;          // + counts and thresholds
-  static constexpr int NLD = NI * RB / 16 / 256;                  // 16-B units per thread per chunk
-  static_assert(CAP <= 64 * NSORT && CAP >= 64 + 16 && FLOATS * 4 <= 80 * 1024, "list capacity, 2 WG/CU");
-};
-__device__ __forceinline__ int tk_unit(int row, int u) { return u ^ (4 * (row & 3)); }
-
-__global__ void split_rows_kernel(const float* __restrict__ T, int64_t n, int KP, float scale,
-                                  _Float16* __restrict__ out) {
-  const int64_t tot = n * KP;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
-    float v = T[e] * scale;
-    asm("" : "+v"(v));  // one fp32 rounding, then hi and lo from that value (see lds_put)
-    const _Float16 h = (_Float16)v;
-    const int64_t r = e / KP, c = e % KP;
-    out[r * 2 * KP + c] = h;
-    out[r * 2 * KP + KP + c] = (_Float16)(v - (float)h);
-  }
-}
-
-hipError_t launch_split_rows(const float* T, int64_t n, int KP, float scale, void* out, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  int64_t blocks = (n * KP + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
-  split_rows_kernel<<<(int)blocks, 256, 0, s>>>(T, n, KP, scale, reinterpret_cast<_Float16*>(out));
-  return hipGetLastError();
-}
-
-template <int KP>
-__global__ __launch_bounds__(256, 2) void topk_kernel(TopkArgs a) {
-  using TL = TopkLds<KP>;
-  constexpr int NQ = KP / 32, NI = TL::NI, NJ = TL::NJ, NLD = TL::NLD, RB = TL::RB;
-  constexpr int CAP = TL::CAP, NS = TL::NSORT, UPR = RB / 16;  // 16-B units per dst row
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  char* tch = reinterpret_cast<char*>(smem);                     // [NI][RB], swizzled units
-  float* lsc = smem + TL::CHUNK;                                 // [64][CAP]
-  int* lix = reinterpret_cast<int*>(lsc + TL::LISTS);            // [64][CAP]
-  int* lcnt = lix + TL::LISTS;                                   // [64]
-  float* lthr = reinterpret_cast<float*>(lcnt + 64);             // [64]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, i16 = lane & 15;
-  const int64_t sb = (int64_t)blockIdx.x * 64 + 16 * wave;       // this wave's first src row
-  if (tid < 64) { lcnt[tid] = 0; lthr[tid] = -INFINITY; }
-  // src fragments: lane (i16, g) holds row sb + i16, columns 32q + 8g .. +7, split hi / lo
-  f16x8 uh[NQ], ul[NQ];
-  {
-    const int64_t si = sb + i16;
-    const int srow = si < a.n_src ? a.src_rows[si] : -1;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      f32x4 v0 = zero4(), v1 = zero4();
-      if (srow >= 0) {
-        v0 = ld4(a.S + (int64_t)srow * KP + 32 * q + 8 * g);
-        v1 = ld4(a.S + (int64_t)srow * KP + 32 * q + 8 * g + 4);
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float v = (e < 4 ? v0[e] : v1[e - 4]) * a.ssc;
-        asm("" : "+v"(v));
-        const _Float16 h = (_Float16)v;
-        uh[q][e] = h;
-        ul[q][e] = (_Float16)(v - (float)h);
-      }
-    }
-  }
-  float* wsc = lsc + wave * 16 * CAP;
-  int* wix = lix + wave * 16 * CAP;
-  int* wcnt = lcnt + wave * 16;
-  float* wthr = lthr + wave * 16;
-  const char* Tb = reinterpret_cast<const char*>(a.Tsplit);
-  // chunk loader: 16-B unit e = tid + 256 u of the chunk (row-major, UPR units per row)
-  f32x4 pf[NLD];
-  auto gload = [&](int64_t j0) {
-#pragma unroll
-    for (int u = 0; u < NLD; ++u) {
-      const int e = tid + 256 * u, r = e / UPR, q = e % UPR;
-      const int64_t dj = j0 + r;
-      pf[u] = dj < a.n_dst ? *reinterpret_cast<const f32x4*>(Tb + dj * RB + 16 * q) : zero4();
-    }
-  };
-  auto lput = [&]() {
-#pragma unroll
-    for (int u = 0; u < NLD; ++u) {
-      const int e = tid + 256 * u, r = e / UPR, q = e % UPR;
-      *reinterpret_cast<f32x4*>(tch + r * RB + 16 * tk_unit(r, q)) = pf[u];
-    }
-  };
-  float thr[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};  // rows 4g + r, accumulator units
-  const float rescale = 1.0f / a.unscale;  // a power of two: exact
-  gload(0);
-  for (int64_t j0 = 0; j0 < a.n_dst; j0 += NI) {
-    __syncthreads();  // previous chunk consumed
-    lput();
-    __syncthreads();
-    if (j0 + NI < a.n_dst) gload(j0 + NI);
-    f32x4 acc[NJ];
-#pragma unroll
-    for (int J = 0; J < NJ; ++J) acc[J] = zero4();
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-#pragma unroll
-      for (int J = 0; J < NJ; ++J) {
-        const int row = 16 * J + i16;
-        // hi units 0 .. KP/8-1, lo units KP/8 .. KP/4-1; this lane's 8 columns: unit 4q + g
-        const f16x8 th = *reinterpret_cast<const f16x8*>(tch + row * RB + 16 * tk_unit(row, 4 * q + g));
-        const f16x8 tl = *reinterpret_cast<const f16x8*>(tch + row * RB + 16 * tk_unit(row, KP / 8 + 4 * q + g));
-        acc[J] = mfma_h(uh[q], th, acc[J]);
-        acc[J] = mfma_h(uh[q], tl, acc[J]);
-        acc[J] = mfma_h(ul[q], th, acc[J]);
-      }
-    }
-    // append candidates 16 dst rows at a time (a list holds <= CAP-16 kept + 16 new): lane holds
-    // src rows 4g + r (of this wave's 16), dst j0 + 16J + i16.  Thresholds live in registers in
-    // the scaled units of the accumulators (thr · 2^(ssc+tsc), exact); appends and the compaction
-    // check only run when some lane beats its threshold (rare once the lists have filled).
-    static_for<0, NJ>([&](auto JJ) {
-      constexpr int J = decltype(JJ)::value;
-      bool hit = false;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) hit |= acc[J][r] >= thr[r];
-      if (__any(hit)) {
-        const int64_t dj = j0 + 16 * J + i16;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int sr = 4 * g + r;
-          if (dj < a.n_dst && acc[J][r] >= thr[r]) {
-            const int pos = atomicAdd(&wcnt[sr], 1);
-            wsc[sr * CAP + pos] = acc[J][r] * a.unscale;
-            wix[sr * CAP + pos] = (int)dj;
-          }
-        }
-        WAVE_LDS_SYNC();
-        // compact the rows that could overflow on the next 16 (best 64 kept, threshold = the 64th)
-        const int mycnt = lane < 16 ? wcnt[lane] : 0;
-        unsigned long long full = __ballot(mycnt > CAP - 16);
-        if (full) {
-          while (full) {
-            const int sr = __builtin_ctzll(full);
-            full &= full - 1;
-            const int cnt = rdlane_i(mycnt, sr);
-            float s2[NS];
-            int i2[NS];
-#pragma unroll
-            for (int q = 0; q < NS; ++q) {
-              const int e = lane + 64 * q;
-              s2[q] = e < cnt ? wsc[sr * CAP + e] : -INFINITY;
-              i2[q] = e < cnt ? wix[sr * CAP + e] : -1;
-            }
-            wave_bitonic<NS>(s2, i2);
-            WAVE_LDS_SYNC();
-            wsc[sr * CAP + lane] = s2[0];
-            wix[sr * CAP + lane] = i2[0];
-            if (lane == 63) wthr[sr] = s2[0];
-            if (lane == 0) wcnt[sr] = 64;
-            WAVE_LDS_SYNC();
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) thr[r] = wthr[4 * g + r] * rescale;
-        }
-      }
-    });
-  }
-  // each wave owns its rows' lists: best KC per row
-  for (int sr = 0; sr < 16; ++sr) {
-    const int64_t si = sb + sr;
-    if (si >= a.n_src) break;
-    const int cnt = wcnt[sr];
-    float s2[NS];
-    int i2[NS];
-#pragma unroll
-    for (int h = 0; h < NS; ++h) {
-      const int e = lane + 64 * h;
-      s2[h] = e < cnt ? wsc[sr * CAP + e] : -INFINITY;
-      i2[h] = e < cnt ? wix[sr * CAP + e] : -1;
-    }
-    wave_bitonic<NS>(s2, i2);
-    a.cand[si * TOPK_KC + lane] = i2[0];
-    a.cand_score[si * TOPK_KC + lane] = s2[0];
-  }
-}
-
-// One wave per src row: exact F2J rescoring of the KC candidates, sort, certify, write top-k.
-template <int KP>
-__global__ __launch_bounds__(256) void topk_rescore_kernel(TopkArgs a) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t si = (int64_t)blockIdx.x * 4 + wave;
-  if (si >= a.n_src) return;
-  const int srow = a.src_rows[si];
-  const float* s = a.S + (int64_t)srow * KP;
-  const int ci = a.cand[si * TOPK_KC + lane];
-  const float approx = a.cand_score[si * TOPK_KC + lane];
-  float ex = -INFINITY;
-  if (ci >= 0) ex = f2j_dot(s, a.T + (int64_t)ci * KP, a.kreal);
-  // t = smallest approx score kept (only meaningful when the list is full)
-  float tmin = approx;
-  for (int o = 32; o > 0; o >>= 1) tmin = fminf(tmin, __shfl_xor(tmin, o));
-  const bool full = a.n_dst > TOPK_KC;
-  // ||s||_2 in double for the error bound
-  double nn = 0.0;
-  for (int c = lane; c < a.kreal; c += 64) nn += (double)s[c] * (double)s[c];
-  for (int o = 32; o > 0; o >>= 1) nn += __shfl_xor(nn, o);
-  float sc1[1] = {ex};
-  int ix1[1] = {ci};
-  wave_bitonic<1>(sc1, ix1);
-  const int k = a.k;
-  const float kth = rdlane(sc1[0], k - 1);
-  if (full) {
-    const double u = 5.9604644775390625e-08;  // 2^-24
-    const double kk = (double)(a.kreal + 2);
-    const double gam = kk * u / (1.0 - kk * u);
-    // fp32 accumulation (2γ_{k+2}) + the split-fp16 representation of both operands and the dropped
-    // lo·lo term (4·2^-22) + fp16 subnormal lo parts (2^-30), all relative to ‖s‖·max‖t‖
-    const double rel = 2.0 * gam + 4.0 * 2.384185791015625e-07 + 9.313225746154785e-10;
-    const double e = rel * sqrt(nn) * (double)a.tmax_norm;
-    if (!((double)kth > (double)tmin + e)) {
-      if (lane == 0) a.need_exact[si] = 1;
-    }
-  }
-  if (lane < k) {
-    const int idx = ix1[0];
-    a.out_ids[si * k + lane] = idx >= 0 ? a.dst_ids[idx] : -1;
-    a.out_scores[si * k + lane] = idx >= 0 ? sc1[0] : __int_as_float(0x7fc00000);
-  }
-}
-
-// Exact path: one workgroup (4 waves) per src row, full F2J scan.  Each wave keeps its best 64·P
-// (score desc, id asc) in registers, slots [0, P) sorted, and buffers up to 64·P newcomers in slots
-// [P, 2P); a batch of 64 scores is only buffered when one of them reaches the current 64·P-th best,
-// and a full buffer is merged by one bitonic sort of the 128·P slots.  The four waves' lists are
-// merged at the end.  P = 1 serves the rows the MFMA pre-selection could not certify; P up to 8
-// serves k up to 512 (recommendForAll* with k > 64, no pre-selection).
-template <int KP, int P>
-__global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32_t* rows, int64_t row0) {
-  __shared__ float msc[4][64 * P];
-  __shared__ int mix[4][64 * P];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t si = rows ? rows[row0 + blockIdx.x] : row0 + (int64_t)blockIdx.x;
-  const int srow = a.src_rows[si];
-  const float* s = a.S + (int64_t)srow * KP;
-  float bs[2 * P];
-  int bi[2 * P];
-#pragma unroll
-  for (int h = 0; h < 2 * P; ++h) { bs[h] = -INFINITY; bi[h] = -1; }
-  int nin = 0;                // newcomer batches buffered (wave-uniform)
-  float thr = -INFINITY;      // the kept list's last score once full
-  for (int64_t j0 = (int64_t)wave * 64; j0 < a.n_dst; j0 += 256) {
-    const int64_t dj = j0 + lane;
-    const float sc = dj < a.n_dst ? f2j_dot(s, a.T + dj * KP, a.kreal) : -INFINITY;
-    if (!__any(sc >= thr)) continue;
-    static_for<0, P>([&](auto hh) {
-      constexpr int h = decltype(hh)::value;
-      if (nin == h) { bs[P + h] = sc; bi[P + h] = dj < a.n_dst ? (int)dj : -1; }
-    });
-    if (++nin == P) {
-      wave_bitonic<2 * P>(bs, bi);
-#pragma unroll
-      for (int h = P; h < 2 * P; ++h) { bs[h] = -INFINITY; bi[h] = -1; }
-      nin = 0;
-      thr = rdlane(bs[P - 1], 63);
-    }
-  }
-  wave_bitonic<2 * P>(bs, bi);
-#pragma unroll
-  for (int h = 0; h < P; ++h) {
-    msc[wave][64 * h + lane] = bs[h];
-    mix[wave][64 * h + lane] = bi[h];
-  }
-  __syncthreads();
-  if (wave == 0) {  // fold the other waves' lists in, one bitonic sort of 128·P slots each
-    for (int w = 1; w < 4; ++w) {
-#pragma unroll
-      for (int h = 0; h < P; ++h) { bs[P + h] = msc[w][64 * h + lane]; bi[P + h] = mix[w][64 * h + lane]; }
-      wave_bitonic<2 * P>(bs, bi);
-    }
-#pragma unroll
-    for (int h = 0; h < P; ++h) {
-      const int e = 64 * h + lane;
-      if (e < a.k) {
-        const int idx = bi[h];
-        a.out_ids[si * a.k + e] = idx >= 0 ? a.dst_ids[idx] : -1;
-        a.out_scores[si * a.k + e] = idx >= 0 ? bs[h] : __int_as_float(0x7fc00000);
-      }
-    }
-  }
-}
-
-template <int KP>
-hipError_t launch_topk_kp(const TopkArgs& a, hipStream_t s) {
-  const size_t lds = (size_t)TopkLds<KP>::FLOATS * 4;
-  static const hipError_t attr = allow_lds(topk_kernel<KP>, lds);
-  if (attr != hipSuccess) return attr;
-  topk_kernel<KP><<<(int)((a.n_src + 63) / 64), 256, lds, s>>>(a);
-  topk_rescore_kernel<KP><<<(int)((a.n_src + 3) / 4), 256, 0, s>>>(a);
-  return hipGetLastError();
-}
-
-hipError_t launch_topk(int KP, const TopkArgs& a, hipStream_t s) {
-  if (a.n_src <= 0) return hipSuccess;
-  if (KP == 64) return launch_topk_kp<64>(a, s);
-  if (KP == 128) return launch_topk_kp<128>(a, s);
-  if (KP == 256) return launch_topk_kp<256>(a, s);
-  return hipErrorInvalidValue;
-}
-
-// max_r ||T[r][0..kreal)||_2 (fp64), stored as the bits of a non-negative double
-__global__ void rownorm_max_kernel(const float* __restrict__ T, int64_t n, int KP, int kreal,
-                                   unsigned long long* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  double best = 0.0;
-  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += (int64_t)gridDim.x * 4) {
-    double s2 = 0.0;
-    for (int c = lane; c < kreal; c += 64) s2 += (double)T[r * KP + c] * (double)T[r * KP + c];
-    for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
-    best = fmax(best, s2);
-  }
-  if (lane == 0) atomicMax(out, (unsigned long long)__double_as_longlong(sqrt(best)));
-}
-
-hipError_t launch_rownorm_max(const float* T, int64_t n, int KP, int kreal, unsigned long long* out, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(out, 0, 8, s);
-  if (e != hipSuccess || n <= 0) return e;
-  int64_t blocks = (n + 3) / 4;
-  if (blocks > 4096) blocks = 4096;
-  rownorm_max_kernel<<<(int)blocks, 256, 0, s>>>(T, n, KP, kreal, out);
-  return hipGetLastError();
-}
-
-template <int KP, int P>
-hipError_t topk_exact_p(const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s) {
-  for (int64_t r0 = 0; r0 < n_rows; r0 += max_rows_per_launch(256)) {
-    const int64_t n = std::min<int64_t>(n_rows - r0, max_rows_per_launch(256));
-    topk_exact_kernel<KP, P><<<(int)n, 256, 0, s>>>(a, rows, r0);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
-}
-template <int KP>
-hipError_t topk_exact_kp(const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s) {
-  if (a.k <= 64) return topk_exact_p<KP, 1>(a, rows, n_rows, s);
-  if (a.k <= 128) return topk_exact_p<KP, 2>(a, rows, n_rows, s);
-  if (a.k <= 256) return topk_exact_p<KP, 4>(a, rows, n_rows, s);
-  if (a.k <= TOPK_MAX) return topk_exact_p<KP, 8>(a, rows, n_rows, s);
-  return hipErrorInvalidValue;
-}
-hipError_t launch_topk_exact(int KP, const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s) {
-  if (n_rows <= 0) return hipSuccess;
-  if (KP == 64) return topk_exact_kp<64>(a, rows, n_rows, s);
-  if (KP == 128) return topk_exact_kp<128>(a, rows, n_rows, s);
-  if (KP == 256) return topk_exact_kp<256>(a, rows, n_rows, s);
-  return hipErrorInvalidValue;
 }
 
 }  // namespace albedo

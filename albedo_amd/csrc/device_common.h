@@ -66,6 +66,8 @@ __device__ __forceinline__ float sum16_last(float x) {
 // multi-instruction expansions; the solve tolerance is 1e-4 relative (tests state it)
 __device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+// launches of one workgroup per row are split so that rows x threads stays below 2^31 (AQL grid size)
+inline int64_t max_rows_per_launch(int threads) { return (int64_t(1) << 31) / threads; }
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
@@ -76,6 +78,17 @@ __device__ __forceinline__ f32x4 mfma_h(f16x8 a, f16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// F2J sdot (netlib sdot.f via F2J: float products added left to right, no FMA contraction)
+__device__ __forceinline__ float f2j_dot(const float* __restrict__ x, const float* __restrict__ y, int k) {
+#pragma clang fp contract(off)
+  float acc = 0.f;
+  for (int c = 0; c < k; ++c) {
+    const float p = x[c] * y[c];
+    acc = acc + p;
+  }
+  return acc;
+}
 
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {

@@ -87,7 +87,9 @@ hipError_t launch_init_random(int KP, int kreal, float* X, int64_t n, uint64_t s
 hipError_t launch_predict(int KP, int kreal, const float* U, const float* V, const int32_t* u,
                           const int32_t* v, float* out, int64_t n, hipStream_t s);
 
-// Top-k: approximate (fp32 MFMA) top-KC candidates per src row, then exact F2J rescoring.
+// Top-k (topk.hip): dst rows ordered by descending norm and packed as fp16 (topk_prepare), an MFMA
+// scan with per-row candidate lists and Cauchy-Schwarz early exit, then exact F2J rescoring of the
+// best TOPK_KC candidates with a certification bound (rows that fail it: topk_exact).
 struct TopkArgs {
   const float* S;          // src factors (original basis) [*][KP]
   const float* T;          // dst factors (original basis) [n_dst][KP]
@@ -96,26 +98,37 @@ struct TopkArgs {
   int64_t n_dst;
   const int32_t* dst_ids;  // raw ids of dst rows (ascending with the row index)
   int kreal;
-  int k;                   // requested top-k (<= 64)
+  int k;                   // requested top-k
   float tmax_norm;         // max_j ||T_j||_2 (for the error bound)
-  const void* Tsplit;      // [n_dst][2*KP] fp16: hi then lo halves of T[j]·2^tsc (split_rows)
-  float ssc;               // src rows are split as S[i]·2^ssc (power of two)
-  float unscale;           // 2^-(ssc + tsc): exact rescaling of the split-fp16 scores
-  int32_t* cand;           // [n_src][KC] scratch
-  float* cand_score;       // [n_src][KC] scratch
+  const void* Th;          // [n_chunks * chunk rows][KP] fp16: T[perm[p]]·tsc, zero rows past n_dst
+  const float* head;       // [n_chunks] ||T_{perm[c·chunk]}||, rounded up (0 past n_dst)
+  const uint32_t* perm;    // [n_dst] dst row of scan position p (descending norm)
+  int64_t n_chunks;
+  float ssc, tsc;          // src / dst fp16 scales (powers of two)
+  float unscale;           // 1 / (ssc·tsc): exact rescaling of the MFMA scores
+  float scaled;            // ssc·tsc
+  float* lscore;           // [n_src][TOPK_CAP] candidate lists (approx score, scan position)
+  int32_t* lidx;
+  int32_t* lcnt;           // [n_src] list lengths
   int32_t* out_ids;        // [n_src][k] raw dst ids
   float* out_scores;       // [n_src][k]
   int32_t* need_exact;     // [n_src] set when the candidate set could not be certified
+  unsigned long long* scanned;  // += dst chunks scanned by each scan workgroup (or null)
 };
-hipError_t launch_topk(int KP, const TopkArgs& a, hipStream_t s);
+constexpr int TOPK_KC = 64;     // candidates rescored exactly per src row (k <= 64)
+constexpr int TOPK_CAP = 256;   // candidate list capacity per src row during the scan
+constexpr int TOPK_MAX = 512;   // k above TOPK_KC: exact full scan (topk_exact_kernel)
+int topk_chunk_rows(int KP);    // dst rows per scan chunk (Th / head are padded to whole chunks)
+size_t topk_sort_temp_bytes(int64_t n_dst);
+// keys: 2·n_dst uint32, perm: 2·n_dst uint32 (perm[0, n_dst) is the result), Th / head as above
+hipError_t topk_prepare(int KP, int kreal, const float* T, int64_t n_dst, float tsc, void* temp, size_t temp_bytes,
+                        uint32_t* keys, uint32_t* perm, void* Th, float* head, hipStream_t s);
+hipError_t launch_topk(int KP, const TopkArgs& a, int n_cu, hipStream_t s);
+int topk_rows_per_workgroup(int KP, int64_t n_src, int n_cu);
 // exact full scan for the given src-row indices (rows == null: rows 0 .. n_rows-1), any k <= TOPK_MAX
 hipError_t launch_topk_exact(int KP, const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s);
-// out[r] = (hi, lo) fp16 split of T[r]·scale: [n][2*KP] halves (scale a power of two)
-hipError_t launch_split_rows(const float* T, int64_t n, int KP, float scale, void* out, hipStream_t s);
 // *out = bits of max_r ||T[r][0..kreal)||_2 computed in fp64
 hipError_t launch_rownorm_max(const float* T, int64_t n, int KP, int kreal, unsigned long long* out, hipStream_t s);
-constexpr int TOPK_KC = 64;     // candidates kept per src row by the MFMA pass (k <= 64)
-constexpr int TOPK_MAX = 512;   // k above TOPK_KC: exact full scan (topk_exact_kernel)
 
 // Ingest (ingest.hip): COO -> remap + CSR.
 struct DeviceBuf;

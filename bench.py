@@ -177,7 +177,7 @@ def main():
             traffic = float(sum(found))
 
     # ---- top-30 users/s (secondary metric; a bounded user subset) ------------------------------
-    topk_ups = None
+    topk_ups = topk_info = None
     if args.topk_users > 0 and world == 1:
         ids = np.empty(n_users, np.int32)
         L.check(lib.als_get_ids(h, 0, L.ptr(ids, C.c_int32)))
@@ -186,10 +186,20 @@ def main():
         out_s = np.empty((sub.size, 30), np.float32)
         L.check(lib.als_recommend(h, 0, 30, L.ptr(sub[:1024], C.c_int32), min(1024, sub.size), None,
                                   L.ptr(out_i, C.c_int32), L.ptr(out_s, C.c_float)))  # warm
+        st0 = np.zeros(4, np.int64)
+        L.check(lib.als_topk_stats(h, L.ptr(st0, C.c_int64)))
         t1 = time.perf_counter()
         L.check(lib.als_recommend(h, 0, 30, L.ptr(sub, C.c_int32), sub.size, None, L.ptr(out_i, C.c_int32),
                                   L.ptr(out_s, C.c_float)))
-        topk_ups = sub.size / (time.perf_counter() - t1)
+        topk_s = time.perf_counter() - t1
+        topk_ups = sub.size / topk_s
+        st1 = np.zeros(4, np.int64)
+        L.check(lib.als_topk_stats(h, L.ptr(st1, C.c_int64)))
+        dst = st1 - st0
+        topk_info = {"users": int(sub.size), "seconds": topk_s, "exact_rescan_rows": int(dst[1]),
+                     "dst_chunks_scanned_frac": float(dst[2]) / max(1, int(dst[3])),
+                     "note": "wall time of als_recommend(k=30) on the user subset: dst norm sort + fp16 pack, "
+                             "MFMA scan with norm-order early exit, exact F2J rescoring, D2H of the lists"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -215,6 +225,7 @@ def main():
                          "kernel_ms_per_sweep": d["ms"]},
             "cpu_baseline": cpu,
             "topk30_users_per_s": topk_ups,
+            "topk30": topk_info,
             "stages_ms_per_sweep": {f"{'user' if s == 0 else 'item'}_{n}": round((stage[s][i] / args.steps), 3)
                                     for s in (0, 1) for i, n in enumerate(L.T_NAMES[:7])},
             "paths": {"user": stats[0].tolist(), "item": stats[1].tolist()},

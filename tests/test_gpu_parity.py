@@ -364,6 +364,41 @@ def test_topk_large_catalogue_bit_exact(gpu_lib, rank, num):
         gpu_lib.als_destroy(h)
 
 
+@pytest.mark.parametrize("rank,n_u", [(50, 300000), (100, 300000), (200, 140000)])
+def test_topk_register_blocking_and_norm_pruning(gpu_lib, rank, n_u):
+    """Src counts large enough for the 512- and 256-row scan workgroups (4 waves x 8 / 4 groups of 16
+    rows), a catalogue with the skewed norms of trained implicit-ALS factors (so the descending-norm
+    scan ends early), ids and score bits of a sample of rows against the F2J-order oracle; the scan
+    counters show the early exit and the certification misses stay rare."""
+    from albedo_amd import _lib as L
+    rng = np.random.default_rng(rank + 1)
+    n_i, num = 20000, 30
+    uid = np.arange(n_u, dtype=np.int32) * 3 + 1
+    iid = rng.permutation(np.arange(n_i, dtype=np.int32) * 2 + 7).astype(np.int32)
+    uf = (rng.standard_normal((n_u, rank)) * rng.lognormal(0.0, 0.5, (n_u, 1))).astype(np.float32)
+    itf = (rng.standard_normal((n_i, rank)) * rng.lognormal(0.0, 1.0, (n_i, 1))).astype(np.float32)
+    itf[n_i - 300:] = itf[:300]  # exact ties across the norm order
+    h = C.c_void_p()
+    L.check(gpu_lib.als_model_create(rank, n_u, L.ptr(uid, C.c_int32), L.ptr(uf, C.c_float), n_i,
+                                     L.ptr(iid, C.c_int32), L.ptr(itf, C.c_float), -1, C.byref(h)))
+    try:
+        ids = np.empty((n_u, num), np.int32)
+        sc = np.empty((n_u, num), np.float32)
+        L.check(gpu_lib.als_recommend(h, 0, num, None, n_u, None, L.ptr(ids, C.c_int32), L.ptr(sc, C.c_float)))
+        st = np.zeros(4, np.int64)
+        L.check(gpu_lib.als_topk_stats(h, L.ptr(st, C.c_int64)))
+        assert st[0] == n_u
+        assert st[1] <= n_u // 100, f"certification misses {st[1]} of {n_u}"
+        assert 0 < st[2] < st[3], f"scan chunks {st[2]} of {st[3]}: no early exit"
+        samp = np.sort(rng.choice(n_u, 600, replace=False))
+        samp[:4] = [0, 1, n_u - 2, n_u - 1]
+        ref_ids, ref_sc = O.recommend_for_all(uid[samp], uf[samp], iid, itf, num)
+        assert np.array_equal(ids[samp], ref_ids)
+        assert np.array_equal(sc[samp].view(np.uint32), ref_sc.view(np.uint32))
+    finally:
+        gpu_lib.als_destroy(h)
+
+
 @pytest.mark.parametrize("num", [100, 300])
 def test_topk_above_64_exact_scan(gpu_lib, num):
     """k > 64 (Spark's recommendForAllUsers takes any k): exact full-scan path, ids and F2J score
