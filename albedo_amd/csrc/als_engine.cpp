@@ -1258,21 +1258,34 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   Side& T = c->s[dst];
   const int KP = c->KP;
   const int64_t nq = subset ? n_subset : S.n;
+  // id -> row: a merge walk when the subset is ascending (the usual case), binary search otherwise
   std::vector<int32_t> qrow(nq);
-  for (int64_t i = 0; i < nq; ++i) qrow[i] = subset ? (int32_t)find_row(S, subset[i]) : (int32_t)i;
+  if (!subset) {
+    for (int64_t i = 0; i < nq; ++i) qrow[i] = (int32_t)i;
+  } else if (std::is_sorted(subset, subset + nq)) {
+    int64_t r = 0;
+    for (int64_t i = 0; i < nq; ++i) {
+      while (r < S.n && S.ids[r] < subset[i]) ++r;
+      qrow[i] = (r < S.n && S.ids[r] == subset[i]) ? (int32_t)r : -1;
+    }
+  } else {
+    for (int64_t i = 0; i < nq; ++i) qrow[i] = (int32_t)find_row(S, subset[i]);
+  }
   if (src_ids_out)
     for (int64_t i = 0; i < nq; ++i) src_ids_out[i] = subset ? subset[i] : S.ids[i];
-  for (int64_t i = 0; i < nq * k; ++i) {
-    dst_ids_out[i] = -1;
-    scores_out[i] = NAN;
-  }
   std::vector<int32_t> known;
   std::vector<int64_t> pos;
+  known.reserve(nq);
+  pos.reserve(nq);
   for (int64_t i = 0; i < nq; ++i)
     if (qrow[i] >= 0) {
       known.push_back(qrow[i]);
       pos.push_back(i);
+    } else {
+      std::fill(dst_ids_out + i * k, dst_ids_out + (i + 1) * k, -1);
+      std::fill(scores_out + i * k, scores_out + (i + 1) * k, NAN);
     }
+  const bool dense_out = (int64_t)known.size() == nq;  // results land in place, no scatter
   if (known.empty() || T.n == 0) return ALS_OK;
   // max row norms (error bound of the pre-selection; fp16 split scales), on the device
   double tmax = 0.0, smax = 0.0;
@@ -1376,14 +1389,20 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
         HIPCHK(launch_topk_exact(KP, a, d_flag.as<int32_t>(), (int64_t)flagged.size(), c->st));
       }
     }
-    std::vector<int32_t> oid(nc * k);
-    std::vector<float> osc(nc * k);
-    HIPCHK(hipMemcpyAsync(oid.data(), d_oid.p, oid.size() * 4, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipMemcpyAsync(osc.data(), d_osc.p, osc.size() * 4, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
-    for (int64_t i = 0; i < nc; ++i) {
-      std::memcpy(dst_ids_out + pos[q0 + i] * k, &oid[i * k], k * 4);
-      std::memcpy(scores_out + pos[q0 + i] * k, &osc[i * k], k * 4);
+    if (dense_out) {
+      HIPCHK(hipMemcpyAsync(dst_ids_out + q0 * k, d_oid.p, nc * k * 4, hipMemcpyDeviceToHost, c->st));
+      HIPCHK(hipMemcpyAsync(scores_out + q0 * k, d_osc.p, nc * k * 4, hipMemcpyDeviceToHost, c->st));
+      HIPCHK(hipStreamSynchronize(c->st));
+    } else {
+      std::vector<int32_t> oid(nc * k);
+      std::vector<float> osc(nc * k);
+      HIPCHK(hipMemcpyAsync(oid.data(), d_oid.p, oid.size() * 4, hipMemcpyDeviceToHost, c->st));
+      HIPCHK(hipMemcpyAsync(osc.data(), d_osc.p, osc.size() * 4, hipMemcpyDeviceToHost, c->st));
+      HIPCHK(hipStreamSynchronize(c->st));
+      for (int64_t i = 0; i < nc; ++i) {
+        std::memcpy(dst_ids_out + pos[q0 + i] * k, &oid[i * k], k * 4);
+        std::memcpy(scores_out + pos[q0 + i] * k, &osc[i * k], k * 4);
+      }
     }
   }
   return ALS_OK;

@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include "device_common.h"
 #include "kernels.h"
 
@@ -141,7 +142,11 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
 
   // src fragments: lane (i16, g) holds row 16gi + i16, columns 32q + 8g .. +7 (fp16, ·ssc)
   f16x8 sf[G][NQ];
-  float thr[G][4];  // rows 16gi + 4g + r, scaled units (+inf: no row)
+  // minus the thresholds of rows 16gi + 4g + r in scaled units, in the MFMA C/D layout: every tile's
+  // accumulation starts from them, so acc = score - threshold and a hit is acc >= 0 (one max over the
+  // tile's accumulators instead of a compare per element).  No row: -inf.  Before a row's first
+  // compaction: minus a lower bound of every score (-1.01·‖ŝ‖·max‖t̂‖ - 1), so every dst row passes.
+  f32x4 nthr[G];
 #pragma unroll
   for (int gi = 0; gi < G; ++gi) {
     const int64_t si = rb0 + wr0 + 16 * gi + i16;
@@ -170,10 +175,14 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
   }
   if (tid < 8) s_flag[tid] = 0;
   __syncthreads();  // no DMA in flight yet: a plain barrier
+  const float tmax_sc = a.tmax_norm * a.tsc;
 #pragma unroll
   for (int gi = 0; gi < G; ++gi)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) thr[gi][r] = s_thr[wr0 + 16 * gi + 4 * g + r];
+    for (int r = 0; r < 4; ++r) {
+      const int wrow = wr0 + 16 * gi + 4 * g + r;
+      nthr[gi][r] = s_thr[wrow] > 0.f ? -INFINITY : 1.01f * s_nrm[wrow] * a.ssc * tmax_sc + 1.f;
+    }
 
   // DMA of chunk c into ring slot `slot`: the wave's DPW KiB of rows (source addresses carry the
   // unit swizzle, the LDS image is lane-linear), then the chunk's head norm (every lane the same word)
@@ -198,12 +207,12 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
   // LDS write beside an LDS-DMA in flight makes it drain the DMA queue first).  Lists above CAP - 16
   // are compacted to their best 64.
   auto check_tile = [&](const f32x4 (&acc)[G], int64_t jt) __attribute__((always_inline)) {
-    bool hit = false;
+    float mx = acc[0][0];
 #pragma unroll
     for (int gi = 0; gi < G; ++gi)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) hit |= acc[gi][r] >= thr[gi][r];
-    if (!__any(hit)) return;
+      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[gi][r]);
+    if (!__any(mx >= 0.f)) return;
     const int64_t dj = jt + i16;
     const bool dv = dj < a.n_dst;
     const uint32_t below = (1u << i16) - 1u;
@@ -212,7 +221,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
     for (int gi = 0; gi < G; ++gi)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const bool p = dv && acc[gi][r] >= thr[gi][r];
+        const bool p = dv && acc[gi][r] >= 0.f;
         const uint64_t m = __ballot(p);
         if (m) {
           const uint32_t mg = (uint32_t)(m >> (16 * g)) & 0xffffu;
@@ -220,7 +229,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
           const int cnt = s_cnt[wrow];
           if (p) {
             const int64_t li = (rb0 + wrow) * CAP + cnt + __popc(mg & below);
-            a.lscore[li] = acc[gi][r] * a.unscale;
+            a.lscore[li] = (acc[gi][r] - nthr[gi][r]) * a.unscale;  // score = acc + threshold
             a.lidx[li] = (int)dj;
           }
           const int ncnt = cnt + __popc(mg);
@@ -266,7 +275,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * gi + 4 * g + r;
         const bool done = row < 64 ? ((d0 >> row) & 1) : ((d1 >> (row - 64)) & 1);
-        if (done) thr[gi][r] = s_thr[wr0 + row] * a.scaled;
+        if (done) nthr[gi][r] = -(s_thr[wr0 + row] * a.scaled);
       }
   };
 
@@ -298,9 +307,9 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       constexpr int J = decltype(JJ)::value;
       if constexpr (J + 1 < NJ) rd(J + 1, df[(J + 1) & 1]);
 #pragma unroll
-      for (int gi = 0; gi < G; ++gi) acc[J & 1][gi] = zero4();
+      for (int gi = 0; gi < G; ++gi) acc[J & 1][gi] = mfma_h(sf[gi][0], df[J & 1][0], nthr[gi]);
 #pragma unroll
-      for (int q = 0; q < NQ; ++q)
+      for (int q = 1; q < NQ; ++q)
 #pragma unroll
         for (int gi = 0; gi < G; ++gi) acc[J & 1][gi] = mfma_h(sf[gi][q], df[J & 1][q], acc[J & 1][gi]);
       if constexpr (J > 0) check_tile(acc[(J - 1) & 1], j0 + 16 * (J - 1));
@@ -358,11 +367,12 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
   const float kth = rdlane(sc1[0], k - 1);
   if (a.n_dst > TOPK_KC) {
     // |F2J(s,t) - approx| <= fp16 rounding of both operands (2^-11 relative, 2^-25 absolute in the
-    // scaled units) + fp32 accumulation of the MFMA and of F2J (γ_{KP+2} each), relative to ‖s‖·max‖t‖
+    // scaled units) + fp32 accumulation of the MFMA started from -threshold (|threshold| <= 1.01·‖s‖·max‖t‖
+    // + 1 scaled unit) and the add-back (4γ_{KP+2}) + F2J's own rounding (γ_{KP+2}), relative to ‖s‖·max‖t‖
     const double u = 5.9604644775390625e-08;  // 2^-24
     const double kk = (double)(KP + 2);
     const double gam = kk * u / (1.0 - kk * u);
-    const double rel = (9.765625e-04 + 2.384185791015625e-07 + 2.0 * gam) * (1.0 + 1.0 / 512.0);
+    const double rel = (9.765625e-04 + 2.384185791015625e-07 + 6.0 * gam) * (1.0 + 1.0 / 512.0);
     const double ns = sqrt(nn), tm = (double)a.tmax_norm;
     const double absu = 2.98023223876953125e-08 * 1.001 * sqrt((double)KP) *
                         (ns / (double)a.tsc + tm / (double)a.ssc) + (double)KP * 8.9e-16 * (double)a.unscale;
@@ -519,7 +529,11 @@ hipError_t launch_scan(const TopkArgs& a, hipStream_t s) {
 // src rows per scan workgroup: the largest register blocking (G = 8 at KP <= 128, 4 at KP = 256)
 // that still gives every CU two workgroups, down to G = 2
 int topk_rows_per_workgroup(int KP, int64_t n_src, int n_cu) {
-  const int gmax = KP <= 128 ? 8 : 4;
+  int gmax = KP <= 128 ? 8 : 4;
+  if (const char* e = std::getenv("ALBEDO_TOPK_GMAX")) {  // experiments: cap the register blocking
+    const int v = std::atoi(e);
+    if (v == 2 || v == 4 || v == 8) gmax = std::min(gmax, v);
+  }
   for (int G = gmax; G > 2; G /= 2)
     if (n_src >= (int64_t)2 * n_cu * 64 * G) return 64 * G;
   return 128;
