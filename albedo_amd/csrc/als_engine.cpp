@@ -1326,7 +1326,7 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   HIPCHK(d_dstids.ensure(T.n * 4));
   HIPCHK(hipMemcpyAsync(d_dstids.p, T.ids.data(), T.n * 4, hipMemcpyHostToDevice, c->st));
   const int64_t chunk = 1 << 20;
-  DevBuf d_src, d_ls, d_li, d_lc, d_oid, d_osc, d_need, d_flag, d_scan;
+  DevBuf d_src, d_ls, d_li, d_lc, d_oid, d_osc, d_need, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp;
   HIPCHK(d_scan.ensure(8));
   for (int64_t q0 = 0; q0 < (int64_t)known.size(); q0 += chunk) {
     const int64_t nc = std::min<int64_t>(chunk, (int64_t)known.size() - q0);
@@ -1370,7 +1370,22 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
     if (exact_only) {
       HIPCHK(launch_topk_exact(KP, a, nullptr, nc, c->st));
     } else {
-      HIPCHK(launch_topk(KP, a, c->n_cu, c->st));
+      // scan order: rows that stop at similar depths share a workgroup (topk_order); the select
+      // writes each row's results back to its own slot
+      TopkArgs b = a;
+      const char* oe = std::getenv("ALBEDO_TOPK_ORDER");
+      if (!(oe && std::atoi(oe) == 0)) {
+        HIPCHK(d_okeys.ensure(nc * 8));
+        HIPCHK(d_order.ensure(nc * 8));
+        HIPCHK(d_srcs.ensure(nc * 4));
+        const size_t otb = topk_order_temp_bytes(nc);
+        HIPCHK(d_otmp.ensure(std::max<size_t>(otb, 16)));
+        HIPCHK(topk_order(KP, a, d_otmp.p, otb, d_okeys.as<uint32_t>(), d_order.as<uint32_t>(), d_srcs.as<int32_t>(),
+                          c->st));
+        b.src_rows = d_srcs.as<int32_t>();
+        b.out_pos = d_order.as<uint32_t>();
+      }
+      HIPCHK(launch_topk(KP, b, c->n_cu, c->st));
       std::vector<int32_t> need(nc);
       HIPCHK(hipMemcpyAsync(need.data(), d_need.p, nc * 4, hipMemcpyDeviceToHost, c->st));
       HIPCHK(hipStreamSynchronize(c->st));

@@ -114,6 +114,7 @@ struct TopkArgs {
   float* out_scores;       // [n_src][k]
   int32_t* need_exact;     // [n_src] set when the candidate set could not be certified
   unsigned long long* scanned;  // += dst chunks scanned by each scan workgroup (or null)
+  const uint32_t* out_pos;      // select: results of scan position i go to slot out_pos[i] (or i)
 };
 constexpr int TOPK_KC = 64;     // candidates rescored exactly per src row (k <= 64)
 constexpr int TOPK_CAP = 256;   // candidate list capacity per src row during the scan
@@ -124,6 +125,12 @@ size_t topk_sort_temp_bytes(int64_t n_dst);
 hipError_t topk_prepare(int KP, int kreal, const float* T, int64_t n_dst, float tsc, void* temp, size_t temp_bytes,
                         uint32_t* keys, uint32_t* perm, void* Th, float* head, hipStream_t s);
 hipError_t launch_topk(int KP, const TopkArgs& a, int n_cu, hipStream_t s);
+// scan order of the src rows (rows that stop at similar depths share a workgroup): keys / order hold
+// 2·n_src uint32 each; order[0, n_src) = the original position of scan position i, src_sorted[i] =
+// a.src_rows[order[i]] (needs a.S, a.T, a.perm, a.src_rows, a.n_src, a.n_dst)
+size_t topk_order_temp_bytes(int64_t n_src);
+hipError_t topk_order(int KP, const TopkArgs& a, void* temp, size_t temp_bytes, uint32_t* keys, uint32_t* order,
+                      int32_t* src_sorted, hipStream_t s);
 int topk_rows_per_workgroup(int KP, int64_t n_src, int n_cu);
 // exact full scan for the given src-row indices (rows == null: rows 0 .. n_rows-1), any k <= TOPK_MAX
 hipError_t launch_topk_exact(int KP, const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s);

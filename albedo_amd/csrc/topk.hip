@@ -29,6 +29,16 @@
 namespace albedo {
 
 typedef __attribute__((address_space(3))) void* tk_lds_vp;
+inline int tk_grid(int64_t n, int per) {
+  int64_t b = (n + per - 1) / per;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(b, 8192));
+}
+size_t topk_sort_temp_bytes(int64_t n);
+__global__ void topk_gather_rows_kernel(const int32_t* __restrict__ rows, const uint32_t* __restrict__ order,
+                                        int64_t n, int32_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = rows[order[i]];
+}
 typedef __attribute__((address_space(1))) const void* tk_glb_vp;
 
 // ---------------------------------------------------------------------------------------------
@@ -341,6 +351,7 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t si = (int64_t)blockIdx.x * 4 + wave;
   if (si >= a.n_src) return;
+  const int64_t so = a.out_pos ? (int64_t)a.out_pos[si] : si;  // output slot of scan position si
   const int srow = a.src_rows[si];
   const float* s = a.S + (int64_t)srow * KP;
   const int cnt = min(a.lcnt[si], CAP);
@@ -378,14 +389,80 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
                         (ns / (double)a.tsc + tm / (double)a.ssc) + (double)KP * 8.9e-16 * (double)a.unscale;
     const double e = rel * ns * tm + absu;
     if (!((double)kth > (double)t + e)) {
-      if (lane == 0) a.need_exact[si] = 1;
+      if (lane == 0) a.need_exact[so] = 1;
     }
   }
   if (lane < k) {
     const int idx = ix1[0];
-    a.out_ids[si * k + lane] = idx >= 0 ? a.dst_ids[idx] : -1;
-    a.out_scores[si * k + lane] = idx >= 0 ? sc1[0] : __int_as_float(0x7fc00000);
+    a.out_ids[so * k + lane] = idx >= 0 ? a.dst_ids[idx] : -1;
+    a.out_scores[so * k + lane] = idx >= 0 ? sc1[0] : __int_as_float(0x7fc00000);
   }
+}
+
+// Scan order of the src rows.  A workgroup's scan ends when its slowest row can stop, so rows that
+// stop at similar depths go together: key = t64 / ‖s‖ with t64 the 64th best score against the 256
+// largest-norm dst rows (a lower bound of the row's final threshold; the row can stop once
+// ‖t_j‖ <= threshold / ‖s‖, so a larger key stops earlier).  One wave per row, fp32, any order (only
+// an ordering key).  keys: order-preserving uint of the float, sorted descending (rocprim) with the
+// row positions as values.
+template <int KP>
+__global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_t* __restrict__ key,
+                                                             uint32_t* __restrict__ val) {
+  const int lane = threadIdx.x & 63;
+  const int64_t si = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (si >= a.n_src) return;
+  const float* s = a.S + (int64_t)a.src_rows[si] * KP;
+  float sc[4];
+  int ix[4];
+  float nn = 0.f;
+  for (int c = lane; c < KP; c += 64) nn = fmaf(s[c], s[c], nn);
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const int p = lane + 64 * h;
+    float v = -INFINITY;
+    if (p < a.n_dst) {
+      const float* t = a.T + (int64_t)a.perm[p] * KP;
+      v = 0.f;
+      for (int c = 0; c < KP; c += 4) {
+        const f32x4 x = ld4(s + c), y = ld4(t + c);
+        v = fmaf(x[0], y[0], fmaf(x[1], y[1], fmaf(x[2], y[2], fmaf(x[3], y[3], v))));
+      }
+    }
+    sc[h] = v;
+    ix[h] = p;
+  }
+  for (int o = 32; o > 0; o >>= 1) nn += __shfl_xor(nn, o);
+  wave_bitonic<4>(sc, ix);
+  const float t64 = rdlane(sc[0], 63);
+  if (lane == 0) {
+    const float k = nn > 0.f ? t64 / sqrtf(nn) : INFINITY;
+    const uint32_t b = __float_as_uint(k);
+    key[si] = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    val[si] = (uint32_t)si;
+  }
+}
+
+size_t topk_order_temp_bytes(int64_t n_src) { return topk_sort_temp_bytes(n_src); }
+
+// src_sorted[i] = src_rows[order[i]], order[i] = the position whose results slot i fills
+hipError_t topk_order(int KP, const TopkArgs& a, void* temp, size_t temp_bytes, uint32_t* keys, uint32_t* order,
+                      int32_t* src_sorted, hipStream_t s) {
+  const int64_t n = a.n_src;
+  if (n <= 0) return hipSuccess;
+  uint32_t* k0 = keys;
+  uint32_t* k1 = keys + n;
+  uint32_t* v0 = order + n;
+  const int blocks = (int)((n + 3) / 4);
+  if (KP == 64) topk_order_key_kernel<64><<<blocks, 256, 0, s>>>(a, k0, v0);
+  else if (KP == 128) topk_order_key_kernel<128><<<blocks, 256, 0, s>>>(a, k0, v0);
+  else topk_order_key_kernel<256><<<blocks, 256, 0, s>>>(a, k0, v0);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  size_t tb = temp_bytes;
+  e = rocprim::radix_sort_pairs_desc(temp, tb, k0, k1, v0, order, (size_t)n, 0, 32, s);
+  if (e != hipSuccess) return e;
+  topk_gather_rows_kernel<<<tk_grid(n, 256), 256, 0, s>>>(a.src_rows, order, n, src_sorted);
+  return hipGetLastError();
 }
 
 // Exact path: one workgroup (4 waves) per src row, full F2J scan.  Each wave keeps its best 64·P
@@ -480,10 +557,6 @@ __global__ void topk_pack_kernel(const float* __restrict__ T, int64_t n, int64_t
 }
 
 namespace {
-inline int tk_grid(int64_t n, int per) {
-  int64_t b = (n + per - 1) / per;
-  return (int)std::max<int64_t>(1, std::min<int64_t>(b, 8192));
-}
 template <int KP>
 constexpr int tk_chunk_rows() { return TkScan<KP, 2>::CH; }
 }  // namespace
