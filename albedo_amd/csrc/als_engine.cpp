@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
+#include <functional>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -1326,7 +1327,7 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   HIPCHK(d_dstids.ensure(T.n * 4));
   HIPCHK(hipMemcpyAsync(d_dstids.p, T.ids.data(), T.n * 4, hipMemcpyHostToDevice, c->st));
   const int64_t chunk = 1 << 20;
-  DevBuf d_src, d_ls, d_li, d_lc, d_oid, d_osc, d_need, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp;
+  DevBuf d_src, d_ls, d_li, d_lc, d_oid, d_osc, d_need, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp, d_thr;
   HIPCHK(d_scan.ensure(8));
   for (int64_t q0 = 0; q0 < (int64_t)known.size(); q0 += chunk) {
     const int64_t nc = std::min<int64_t>(chunk, (int64_t)known.size() - q0);
@@ -1373,6 +1374,7 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
       // scan order: rows that stop at similar depths share a workgroup (topk_order); the select
       // writes each row's results back to its own slot
       TopkArgs b = a;
+      if (const char* de = std::getenv("ALBEDO_TOPK_DRAIN")) b.drain = std::atoi(de);
       const char* oe = std::getenv("ALBEDO_TOPK_ORDER");
       if (!(oe && std::atoi(oe) == 0)) {
         HIPCHK(d_okeys.ensure(nc * 8));
@@ -1380,12 +1382,52 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
         HIPCHK(d_srcs.ensure(nc * 4));
         const size_t otb = topk_order_temp_bytes(nc);
         HIPCHK(d_otmp.ensure(std::max<size_t>(otb, 16)));
+        HIPCHK(d_thr.ensure(nc * 8));
         HIPCHK(topk_order(KP, a, d_otmp.p, otb, d_okeys.as<uint32_t>(), d_order.as<uint32_t>(), d_srcs.as<int32_t>(),
-                          c->st));
+                          d_thr.as<float>(), d_thr.as<float>() + nc, c->st));
         b.src_rows = d_srcs.as<int32_t>();
         b.out_pos = d_order.as<uint32_t>();
+        b.thr0 = d_thr.as<float>() + nc;
+        if (const char* te = std::getenv("ALBEDO_TOPK_THR0"); te && std::atoi(te) == 0) b.thr0 = nullptr;
       }
       HIPCHK(launch_topk(KP, b, c->n_cu, c->st));
+      if (const char* dbg = std::getenv("ALBEDO_TOPK_DEBUG"); dbg && std::atoi(dbg) > 0) {  // diagnostics
+        std::vector<int32_t> lc(nc), nd(nc);
+        std::vector<float> t0(nc);
+        std::vector<uint32_t> od(nc);
+        HIPCHK(hipStreamSynchronize(c->st));
+        HIPCHK(hipMemcpy(lc.data(), d_lc.p, nc * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(nd.data(), d_need.p, nc * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(t0.data(), d_thr.as<float>() + nc, nc * 4, hipMemcpyDeviceToHost));
+        if (b.out_pos) HIPCHK(hipMemcpy(od.data(), b.out_pos, nc * 4, hipMemcpyDeviceToHost));
+        int64_t lt64 = 0, nflag = 0, printed = 0;
+        for (int64_t i = 0; i < nc; ++i) {
+          const int64_t o = b.out_pos ? od[i] : i;
+          lt64 += lc[i] < 64;
+          nflag += nd[o] != 0;
+          bool bad = false;
+          if (lc[i] >= 64 && std::getenv("ALBEDO_TOPK_THR0")) {  // thr0 above the scan's own 64th best?
+            std::vector<float> ls(std::min(lc[i], TOPK_CAP));
+            HIPCHK(hipMemcpy(ls.data(), d_ls.as<float>() + i * TOPK_CAP, ls.size() * 4, hipMemcpyDeviceToHost));
+            std::nth_element(ls.begin(), ls.begin() + 63, ls.end(), std::greater<float>());
+            bad = t0[i] > ls[63];
+            if (bad && printed < 8) std::fprintf(stderr, "[topk dbg] pos %lld thr0 %.9g above the scan's 64th %.9g\n",
+                                                 (long long)i, t0[i], ls[63]);
+            lt64 += bad;
+          }
+          if ((nd[o] || bad) && printed < 8) {
+            std::vector<float> ls(std::min(lc[i], TOPK_CAP));
+            HIPCHK(hipMemcpy(ls.data(), d_ls.as<float>() + i * TOPK_CAP, ls.size() * 4, hipMemcpyDeviceToHost));
+            std::sort(ls.begin(), ls.end(), std::greater<float>());
+            std::fprintf(stderr, "[topk dbg] pos %lld (slot %lld) cnt %d thr0 %.9g best %.9g 64th %.9g\n", (long long)i,
+                         (long long)o, lc[i], b.thr0 ? t0[i] : 0.f, ls.empty() ? 0.f : ls[0],
+                         ls.size() >= 64 ? ls[63] : -1.f);
+            ++printed;
+          }
+        }
+        std::fprintf(stderr, "[topk dbg] rows %lld, lists < 64: %lld, flagged %lld\n", (long long)nc, (long long)lt64,
+                     (long long)nflag);
+      }
       std::vector<int32_t> need(nc);
       HIPCHK(hipMemcpyAsync(need.data(), d_need.p, nc * 4, hipMemcpyDeviceToHost, c->st));
       HIPCHK(hipStreamSynchronize(c->st));

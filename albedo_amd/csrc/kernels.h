@@ -115,9 +115,11 @@ struct TopkArgs {
   int32_t* need_exact;     // [n_src] set when the candidate set could not be certified
   unsigned long long* scanned;  // += dst chunks scanned by each scan workgroup (or null)
   const uint32_t* out_pos;      // select: results of scan position i go to slot out_pos[i] (or i)
+  const float* thr0;            // scan: starting threshold of each src position (topk_order; or null)
+  int drain;                    // debug: drain the VM counter every chunk
 };
 constexpr int TOPK_KC = 64;     // candidates rescored exactly per src row (k <= 64)
-constexpr int TOPK_CAP = 256;   // candidate list capacity per src row during the scan
+constexpr int TOPK_CAP = 128;   // candidate list capacity per src row (compacted to 64 above CAP - 16)
 constexpr int TOPK_MAX = 512;   // k above TOPK_KC: exact full scan (topk_exact_kernel)
 int topk_chunk_rows(int KP);    // dst rows per scan chunk (Th / head are padded to whole chunks)
 size_t topk_sort_temp_bytes(int64_t n_dst);
@@ -130,7 +132,7 @@ hipError_t launch_topk(int KP, const TopkArgs& a, int n_cu, hipStream_t s);
 // a.src_rows[order[i]] (needs a.S, a.T, a.perm, a.src_rows, a.n_src, a.n_dst)
 size_t topk_order_temp_bytes(int64_t n_src);
 hipError_t topk_order(int KP, const TopkArgs& a, void* temp, size_t temp_bytes, uint32_t* keys, uint32_t* order,
-                      int32_t* src_sorted, hipStream_t s);
+                      int32_t* src_sorted, float* thr_tmp, float* thr_sorted, hipStream_t s);
 int topk_rows_per_workgroup(int KP, int64_t n_src, int n_cu);
 // exact full scan for the given src-row indices (rows == null: rows 0 .. n_rows-1), any k <= TOPK_MAX
 hipError_t launch_topk_exact(int KP, const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s);

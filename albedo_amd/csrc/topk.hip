@@ -34,10 +34,13 @@ inline int tk_grid(int64_t n, int per) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(b, 8192));
 }
 size_t topk_sort_temp_bytes(int64_t n);
-__global__ void topk_gather_rows_kernel(const int32_t* __restrict__ rows, const uint32_t* __restrict__ order,
-                                        int64_t n, int32_t* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+__global__ void topk_gather_rows_kernel(const int32_t* __restrict__ rows, const float* __restrict__ thr,
+                                        const uint32_t* __restrict__ order, int64_t n, int32_t* __restrict__ out,
+                                        float* __restrict__ thr_out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     out[i] = rows[order[i]];
+    thr_out[i] = thr[order[i]];
+  }
 }
 typedef __attribute__((address_space(1))) const void* tk_glb_vp;
 
@@ -116,6 +119,8 @@ struct TkScan {
 // 16-B unit u of dst row `row` is stored at unit u ^ tk_sw(row): every ds_read_b128 lane group of a
 // fragment read (16 rows x one unit, cdna ds_read_b128 groups) hits 16 distinct 16-B bank slots.
 template <int KP>
+__host__ __device__ constexpr int topk_chunk_rows_dev() { return TkScan<KP, 2>::CH; }
+template <int KP>
 __device__ __forceinline__ int tk_sw(int row) {
   if constexpr (KP == 64) return (row >> 1) & 7;
   else return row & 15;
@@ -138,6 +143,10 @@ template <int KP, int G>
 __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
   using C = TkScan<KP, G>;
   constexpr int NQ = C::NQ, NJ = C::NJ, RB = C::RB, CAP = TOPK_CAP;
+  // a list is compacted to its best 64 once it holds more than TRIG (<= TRIG + 16 <= 64·NSC entries):
+  // frequent enough that the threshold follows the running 64th best
+  constexpr int TRIG = TOPK_CAP - 16, NSC = TOPK_CAP / 64;
+  static_assert(TRIG + 16 <= 64 * NSC && TRIG + 16 <= CAP, "compaction width");
   extern __shared__ __attribute__((aligned(16))) char lds[];  // one LDS object (glds pipelining)
   float* s_thr = reinterpret_cast<float*>(lds + C::NSTG * C::SLOT);  // [RWG] thresholds (unscaled)
   int* s_cnt = reinterpret_cast<int*>(s_thr + C::RWG);                // [RWG] list lengths
@@ -179,7 +188,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
     if (g == 0) {
       const int wrow = wr0 + 16 * gi + i16;
       s_nrm[wrow] = __double2float_ru(sqrt(ss));
-      s_thr[wrow] = srow >= 0 ? -INFINITY : INFINITY;
+      s_thr[wrow] = srow < 0 ? INFINITY : (a.thr0 ? a.thr0[si] : -INFINITY);
       s_cnt[wrow] = 0;
     }
   }
@@ -191,7 +200,9 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int wrow = wr0 + 16 * gi + 4 * g + r;
-      nthr[gi][r] = s_thr[wrow] > 0.f ? -INFINITY : 1.01f * s_nrm[wrow] * a.ssc * tmax_sc + 1.f;
+      const float t0 = s_thr[wrow];
+      nthr[gi][r] = t0 == INFINITY ? -INFINITY
+                  : t0 == -INFINITY ? 1.01f * s_nrm[wrow] * a.ssc * tmax_sc + 1.f : -(t0 * a.scaled);
     }
 
   // DMA of chunk c into ring slot `slot`: the wave's DPW KiB of rows (source addresses carry the
@@ -214,7 +225,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
 
   // candidates of one 16-row tile (dst positions jt .. jt+15).  Slots come from a ballot prefix count
   // over the 16 lanes of a row's group, list lengths are kept in LDS by asm stores (a compiler-visible
-  // LDS write beside an LDS-DMA in flight makes it drain the DMA queue first).  Lists above CAP - 16
+  // LDS write beside an LDS-DMA in flight makes it drain the DMA queue first).  Lists above TRIG
   // are compacted to their best 64.
   auto check_tile = [&](const f32x4 (&acc)[G], int64_t jt) __attribute__((always_inline)) {
     float mx = acc[0][0];
@@ -244,14 +255,14 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
           }
           const int ncnt = cnt + __popc(mg);
           if (i16 == 0 && mg) lds_store_asm(s_cnt + wrow, ncnt);
-          over |= ncnt > CAP - 16;
+          over |= ncnt > TRIG;
         }
       }
     if (!__any(over)) return;
     // wave-local rows to compact: lane l checks rows l and 64 + l
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    uint64_t f0 = __ballot(lane < 16 * G && s_cnt[wr0 + lane] > CAP - 16);
-    uint64_t f1 = (16 * G > 64) ? __ballot(s_cnt[wr0 + 64 + lane] > CAP - 16) : 0ull;
+    uint64_t f0 = __ballot(lane < 16 * G && s_cnt[wr0 + lane] > TRIG);
+    uint64_t f1 = (16 * G > 64) ? __ballot(s_cnt[wr0 + 64 + lane] > TRIG) : 0ull;
     const uint64_t d0 = f0, d1 = f1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's list stores are in L2
     while (f0 | f1) {
@@ -260,15 +271,15 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       else { wl = 64 + __builtin_ctzll(f1); f1 &= f1 - 1; }
       const int cnt = s_cnt[wr0 + wl];
       const int64_t lb = (rb0 + wr0 + wl) * CAP;
-      float s2[CAP / 64];
-      int i2[CAP / 64];
+      float s2[NSC];
+      int i2[NSC];
 #pragma unroll
-      for (int h = 0; h < CAP / 64; ++h) {
+      for (int h = 0; h < NSC; ++h) {
         const int e = lane + 64 * h;
         s2[h] = e < cnt ? agent_load(a.lscore + lb + e) : -INFINITY;
         i2[h] = e < cnt ? agent_load(a.lidx + lb + e) : -1;
       }
-      wave_bitonic<CAP / 64>(s2, i2);
+      wave_bitonic<NSC>(s2, i2);
       a.lscore[lb + lane] = s2[0];
       a.lidx[lb + lane] = i2[0];
       const float t64 = rdlane(s2[0], 63);
@@ -293,7 +304,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
   for (; c < nch; ++c) {
     // this wave's DMAs of chunk c have landed (in-order VM counter; later list stores only make the
     // wait stricter), then one barrier publishes every wave's part and retires slot (c-1) % NSTG
-    if (c + C::NSTG - 2 < nch) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NVM * (C::NSTG - 2)) : "memory");
+    if (c + C::NSTG - 2 < nch && !a.drain) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NVM * (C::NSTG - 2)) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -331,7 +342,9 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       bool ok = true;
       if (lane < 16 * G) ok = s_nrm[wr0 + lane] * hn <= s_thr[wr0 + lane];
       if (16 * G > 64) ok = ok && s_nrm[wr0 + 64 + lane] * hn <= s_thr[wr0 + 64 + lane];
-      const bool done = !__any(!ok);
+      // no vote before the 256 dst rows behind the starting thresholds are scanned (their 64 best
+      // must reach the lists)
+      const bool done = !__any(!ok) && (c + 1) * C::CH >= 256;
       if (lane == 0) lds_store_asm(s_flag + (c & 1) * 4 + wave, done ? 1 : 0);
     }
   }
@@ -367,7 +380,7 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
   const float t = rdlane(s2[0], 63);  // the 64th approximate score (-inf when fewer)
   const int row = i2[0] >= 0 ? a.perm[i2[0]] : -1;
   float ex = -INFINITY;
-  if (row >= 0) ex = f2j_dot(s, a.T + (int64_t)row * KP, a.kreal);
+  if (row >= 0) ex = f2j_dot_v4(s, a.T + (int64_t)row * KP, a.kreal);
   double nn = 0.0;
   for (int c = lane; c < a.kreal; c += 64) nn += (double)s[c] * (double)s[c];
   for (int o = 32; o > 0; o >>= 1) nn += __shfl_xor(nn, o);
@@ -388,7 +401,9 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
     const double absu = 2.98023223876953125e-08 * 1.001 * sqrt((double)KP) *
                         (ns / (double)a.tsc + tm / (double)a.ssc) + (double)KP * 8.9e-16 * (double)a.unscale;
     const double e = rel * ns * tm + absu;
-    if (!((double)kth > (double)t + e)) {
+    // fewer than 64 listed (a scan that stopped before 64 rows reached a starting threshold): the
+    // bound below needs t >= the last threshold, which only a full list guarantees
+    if (cnt < TOPK_KC || !((double)kth > (double)t + e)) {
       if (lane == 0) a.need_exact[so] = 1;
     }
   }
@@ -399,69 +414,116 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
   }
 }
 
-// Scan order of the src rows.  A workgroup's scan ends when its slowest row can stop, so rows that
-// stop at similar depths go together: key = t64 / ‖s‖ with t64 the 64th best score against the 256
-// largest-norm dst rows (a lower bound of the row's final threshold; the row can stop once
-// ‖t_j‖ <= threshold / ‖s‖, so a larger key stops earlier).  One wave per row, fp32, any order (only
-// an ordering key).  keys: order-preserving uint of the float, sorted descending (rocprim) with the
-// row positions as values.
+// Scan order and starting thresholds of the src rows.  A workgroup's scan ends when its slowest row
+// can stop, so rows that stop at similar depths go together.  One wave per 16 src rows scores them
+// against the 256 largest-norm dst rows with the scan's own fp16 operands on MFMA, and v* = the
+// 64th best of those 256 (bisection on order-preserving keys): a lower bound of the row's final
+// 64th best.  thr0 = v* minus the
+// rounding difference between this accumulation and the scan's (8γ_{KP+2}·‖s‖·max‖t‖) is a valid
+// starting threshold: the 64 dst rows above v* reach the list, so the final 64th approximate score
+// is >= thr0.  key = thr0 / ‖s‖: the row can stop once ‖t_j‖ <= threshold / ‖s‖, so a larger key
+// stops earlier (order-preserving uint of the float, sorted descending with the positions as values).
 template <int KP>
 __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_t* __restrict__ key,
-                                                             uint32_t* __restrict__ val) {
-  const int lane = threadIdx.x & 63;
-  const int64_t si = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (si >= a.n_src) return;
-  const float* s = a.S + (int64_t)a.src_rows[si] * KP;
-  float sc[4];
-  int ix[4];
-  float nn = 0.f;
-  for (int c = lane; c < KP; c += 64) nn = fmaf(s[c], s[c], nn);
+                                                             uint32_t* __restrict__ val, float* __restrict__ thr0) {
+  constexpr int NQ = KP / 32, RB = 2 * KP;
+  const int lane = threadIdx.x & 63, g = lane >> 4, i16 = lane & 15;
+  const int64_t sb = (int64_t)blockIdx.x * 64 + (threadIdx.x >> 6) * 16;  // the wave's first position
+  const int64_t si = sb + i16;
+  const int srow = si < a.n_src ? a.src_rows[si] : -1;
+  const float* sp = a.S + (int64_t)(srow >= 0 ? srow : 0) * KP + 8 * g;
+  const float keep = srow >= 0 ? 1.f : 0.f;
+  f16x8 sf[NQ];
+  double ss = 0.0;
 #pragma unroll
-  for (int h = 0; h < 4; ++h) {
-    const int p = lane + 64 * h;
-    float v = -INFINITY;
-    if (p < a.n_dst) {
-      const float* t = a.T + (int64_t)a.perm[p] * KP;
-      v = 0.f;
-      for (int c = 0; c < KP; c += 4) {
-        const f32x4 x = ld4(s + c), y = ld4(t + c);
-        v = fmaf(x[0], y[0], fmaf(x[1], y[1], fmaf(x[2], y[2], fmaf(x[3], y[3], v))));
-      }
+  for (int q = 0; q < NQ; ++q) {
+    const f32x4 v0 = ld4(sp + 32 * q), v1 = ld4(sp + 32 * q + 4);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = (e < 4 ? v0[e] : v1[e - 4]) * keep;
+      ss += (double)v * (double)v;
+      sf[q][e] = (_Float16)(v * a.ssc);
     }
-    sc[h] = v;
-    ix[h] = p;
   }
-  for (int o = 32; o > 0; o >>= 1) nn += __shfl_xor(nn, o);
-  wave_bitonic<4>(sc, ix);
-  const float t64 = rdlane(sc[0], 63);
-  if (lane == 0) {
-    const float k = nn > 0.f ? t64 / sqrtf(nn) : INFINITY;
-    const uint32_t b = __float_as_uint(k);
-    key[si] = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-    val[si] = (uint32_t)si;
+  ss += __shfl_xor(ss, 16);
+  ss += __shfl_xor(ss, 32);  // every lane: ‖s‖² of row i16
+  const char* Th = reinterpret_cast<const char*>(a.Th);
+  const int64_t n_pad = a.n_chunks * (int64_t)topk_chunk_rows_dev<KP>();
+  // order-preserving uint keys of the 256 scores: lane (i16, g) holds column 16J + i16 of rows 4g + r
+  uint32_t u[16][4];
+#pragma unroll
+  for (int J = 0; J < 16; ++J) {
+    const int64_t p = 16 * J + i16;
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      f16x8 d = {};
+      if (p < n_pad) d = *reinterpret_cast<const f16x8*>(Th + p * RB + 16 * (4 * q + g));
+      acc = mfma_h(sf[q], d, acc);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t bb = __float_as_uint(p < a.n_dst ? acc[r] : -INFINITY);
+      u[J][r] = (bb & 0x80000000u) ? ~bb : (bb | 0x80000000u);
+    }
+  }
+  // exact 64th largest per row: bisection on the key (count of keys >= mid over the row's 16 lanes)
+  float vs[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    uint32_t lo = 0u, hi = 0xffffffffu;  // count(>= lo) >= 64 always holds (256 keys >= 0)
+    for (int it = 0; it < 32; ++it) {
+      const uint32_t mid = lo + (uint32_t)(((uint64_t)hi - lo + 1) >> 1);
+      int cnt = 0;
+#pragma unroll
+      for (int J = 0; J < 16; ++J) cnt += u[J][r] >= mid ? 1 : 0;
+      for (int o = 1; o < 16; o <<= 1) cnt += __shfl_xor(cnt, o);
+      if (cnt >= 64) lo = mid;
+      else hi = mid - 1u;
+    }
+    vs[r] = __uint_as_float((lo & 0x80000000u) ? (lo & 0x7fffffffu) : ~lo);
+  }
+  const double nrm = sqrt(__shfl(ss, 4 * g + (i16 & 3)));  // ‖s‖ of row 4g + r (all lanes take part)
+  if (i16 < 4) {
+    const int r = i16;
+    const int64_t pr = sb + 4 * g + r;
+    float v = vs[0];
+#pragma unroll
+    for (int rr = 1; rr < 4; ++rr) v = r == rr ? vs[rr] : v;
+    if (pr < a.n_src) {
+      const double kk = (double)(KP + 2) * 5.9604644775390625e-08;
+      const double margin = (8.0 * kk / (1.0 - kk) + 9.5367431640625e-07) * nrm * (double)a.tmax_norm + 1e-30;
+      const float t0 = v == -INFINITY ? -INFINITY : (float)((double)v * (double)a.unscale - margin);
+      thr0[pr] = t0;
+      const float k = nrm > 0.0 ? (float)((double)t0 / nrm) : INFINITY;
+      const uint32_t bb = __float_as_uint(k);
+      key[pr] = (bb & 0x80000000u) ? ~bb : (bb | 0x80000000u);
+      val[pr] = (uint32_t)pr;
+    }
   }
 }
 
 size_t topk_order_temp_bytes(int64_t n_src) { return topk_sort_temp_bytes(n_src); }
 
-// src_sorted[i] = src_rows[order[i]], order[i] = the position whose results slot i fills
+// src_sorted[i] = src_rows[order[i]], thr_sorted[i] = thr0[order[i]]; order[i] = the position whose
+// results slot i fills
 hipError_t topk_order(int KP, const TopkArgs& a, void* temp, size_t temp_bytes, uint32_t* keys, uint32_t* order,
-                      int32_t* src_sorted, hipStream_t s) {
+                      int32_t* src_sorted, float* thr_tmp, float* thr_sorted, hipStream_t s) {
   const int64_t n = a.n_src;
   if (n <= 0) return hipSuccess;
   uint32_t* k0 = keys;
   uint32_t* k1 = keys + n;
   uint32_t* v0 = order + n;
-  const int blocks = (int)((n + 3) / 4);
-  if (KP == 64) topk_order_key_kernel<64><<<blocks, 256, 0, s>>>(a, k0, v0);
-  else if (KP == 128) topk_order_key_kernel<128><<<blocks, 256, 0, s>>>(a, k0, v0);
-  else topk_order_key_kernel<256><<<blocks, 256, 0, s>>>(a, k0, v0);
+  const int blocks = (int)((n + 63) / 64);
+  if (KP == 64) topk_order_key_kernel<64><<<blocks, 256, 0, s>>>(a, k0, v0, thr_tmp);
+  else if (KP == 128) topk_order_key_kernel<128><<<blocks, 256, 0, s>>>(a, k0, v0, thr_tmp);
+  else topk_order_key_kernel<256><<<blocks, 256, 0, s>>>(a, k0, v0, thr_tmp);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   size_t tb = temp_bytes;
   e = rocprim::radix_sort_pairs_desc(temp, tb, k0, k1, v0, order, (size_t)n, 0, 32, s);
   if (e != hipSuccess) return e;
-  topk_gather_rows_kernel<<<tk_grid(n, 256), 256, 0, s>>>(a.src_rows, order, n, src_sorted);
+  topk_gather_rows_kernel<<<tk_grid(n, 256), 256, 0, s>>>(a.src_rows, thr_tmp, order, n, src_sorted, thr_sorted);
   return hipGetLastError();
 }
 
@@ -487,7 +549,7 @@ __global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32
   float thr = -INFINITY;      // the kept list's last score once full
   for (int64_t j0 = (int64_t)wave * 64; j0 < a.n_dst; j0 += 256) {
     const int64_t dj = j0 + lane;
-    const float sc = dj < a.n_dst ? f2j_dot(s, a.T + dj * KP, a.kreal) : -INFINITY;
+    const float sc = dj < a.n_dst ? f2j_dot_v4(s, a.T + dj * KP, a.kreal) : -INFINITY;
     if (!__any(sc >= thr)) continue;
     static_for<0, P>([&](auto hh) {
       constexpr int h = decltype(hh)::value;
