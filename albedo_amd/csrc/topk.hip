@@ -113,7 +113,7 @@ struct TkScan {
   static constexpr int RWG = 64 * G;             // src rows per workgroup (16·G per wave)
   static constexpr int DPW = CB / 1024 / 4;      // 1-KiB row DMAs per wave per chunk
   static constexpr int NVM = DPW + 1;            // DMA instructions per wave per chunk
-  static constexpr int LDS = NSTG * SLOT + 3 * RWG * 4 + 8 * 4;
+  static constexpr int LDS = NSTG * SLOT + 2 * RWG * 4 + 8 * 4;
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 // 16-B unit u of dst row `row` is stored at unit u ^ tk_sw(row): every ds_read_b128 lane group of a
@@ -146,11 +146,10 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
   // a list is compacted to its best 64 once it holds more than TRIG (<= TRIG + 16 <= 64·NSC entries):
   // frequent enough that the threshold follows the running 64th best
   constexpr int TRIG = TOPK_CAP - 16, NSC = TOPK_CAP / 64;
-  static_assert(TRIG + 16 <= 64 * NSC && TRIG + 16 <= CAP, "compaction width");
+  static_assert(TRIG + 16 <= 64 * NSC && TRIG + 16 <= CAP && TRIG + 16 <= 255, "compaction width, byte counters");
   extern __shared__ __attribute__((aligned(16))) char lds[];  // one LDS object (glds pipelining)
   float* s_thr = reinterpret_cast<float*>(lds + C::NSTG * C::SLOT);  // [RWG] thresholds (unscaled)
-  int* s_cnt = reinterpret_cast<int*>(s_thr + C::RWG);                // [RWG] list lengths
-  float* s_nrm = reinterpret_cast<float*>(s_cnt + C::RWG);            // [RWG] ‖s‖ rounded up
+  float* s_nrm = s_thr + C::RWG;                                      // [RWG] ‖s‖ rounded up
   int* s_flag = reinterpret_cast<int*>(s_nrm + C::RWG);           // [2][4] per-wave "done" votes
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i16 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -166,6 +165,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
   // tile's accumulators instead of a compare per element).  No row: -inf.  Before a row's first
   // compaction: minus a lower bound of every score (-1.01·‖ŝ‖·max‖t̂‖ - 1), so every dst row passes.
   f32x4 nthr[G];
+  uint32_t cntp[G];  // list lengths, one byte per row (see check_tile)
 #pragma unroll
   for (int gi = 0; gi < G; ++gi) {
     const int64_t si = rb0 + wr0 + 16 * gi + i16;
@@ -189,12 +189,13 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       const int wrow = wr0 + 16 * gi + i16;
       s_nrm[wrow] = __double2float_ru(sqrt(ss));
       s_thr[wrow] = srow < 0 ? INFINITY : (a.thr0 ? a.thr0[si] : -INFINITY);
-      s_cnt[wrow] = 0;
     }
   }
   if (tid < 8) s_flag[tid] = 0;
   __syncthreads();  // no DMA in flight yet: a plain barrier
   const float tmax_sc = a.tmax_norm * a.tsc;
+#pragma unroll
+  for (int gi = 0; gi < G; ++gi) cntp[gi] = 0u;
 #pragma unroll
   for (int gi = 0; gi < G; ++gi)
 #pragma unroll
@@ -224,9 +225,9 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
     if (c < nch) dma(c, c);
 
   // candidates of one 16-row tile (dst positions jt .. jt+15).  Slots come from a ballot prefix count
-  // over the 16 lanes of a row's group, list lengths are kept in LDS by asm stores (a compiler-visible
-  // LDS write beside an LDS-DMA in flight makes it drain the DMA queue first).  Lists above TRIG
-  // are compacted to their best 64.
+  // over the 16 lanes of a row's group; list lengths live in registers, one byte per row (cntp[gi]
+  // byte r: row 16gi + 4g + r, the same in the 16 lanes of group g), so the append path touches no
+  // LDS.  Lists above TRIG are compacted to their best 64.
   auto check_tile = [&](const f32x4 (&acc)[G], int64_t jt) __attribute__((always_inline)) {
     float mx = acc[0][0];
 #pragma unroll
@@ -247,29 +248,43 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
         if (m) {
           const uint32_t mg = (uint32_t)(m >> (16 * g)) & 0xffffu;
           const int wrow = wr0 + 16 * gi + 4 * g + r;
-          const int cnt = s_cnt[wrow];
+          const int cnt = (int)((cntp[gi] >> (8 * r)) & 0xffu);
           if (p) {
             const int64_t li = (rb0 + wrow) * CAP + cnt + __popc(mg & below);
             a.lscore[li] = (acc[gi][r] - nthr[gi][r]) * a.unscale;  // score = acc + threshold
             a.lidx[li] = (int)dj;
           }
           const int ncnt = cnt + __popc(mg);
-          if (i16 == 0 && mg) lds_store_asm(s_cnt + wrow, ncnt);
+          cntp[gi] += (uint32_t)__popc(mg) << (8 * r);
           over |= ncnt > TRIG;
         }
       }
     if (!__any(over)) return;
-    // wave-local rows to compact: lane l checks rows l and 64 + l
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    uint64_t f0 = __ballot(lane < 16 * G && s_cnt[wr0 + lane] > TRIG);
-    uint64_t f1 = (16 * G > 64) ? __ballot(s_cnt[wr0 + 64 + lane] > TRIG) : 0ull;
+    // wave-local rows to compact (bit 16gi + 4g + r)
+    uint64_t f0 = 0, f1 = 0;
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint64_t m = __ballot(((cntp[gi] >> (8 * r)) & 0xffu) > (uint32_t)TRIG);
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg)
+          if ((m >> (16 * gg)) & 1) {
+            const int row = 16 * gi + 4 * gg + r;
+            if (row < 64) f0 |= 1ull << row; else f1 |= 1ull << (row - 64);
+          }
+      }
     const uint64_t d0 = f0, d1 = f1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's list stores are in L2
     while (f0 | f1) {
       int wl;
       if (f0) { wl = __builtin_ctzll(f0); f0 &= f0 - 1; }
       else { wl = 64 + __builtin_ctzll(f1); f1 &= f1 - 1; }
-      const int cnt = s_cnt[wr0 + wl];
+      uint32_t cw = 0;  // the row's length: byte (wl & 3) of cntp[wl >> 4] in lane 16·((wl >> 2) & 3)
+#pragma unroll
+      for (int gi = 0; gi < G; ++gi)
+        if ((wl >> 4) == gi) cw = (uint32_t)rdlane_i((int)cntp[gi], 16 * ((wl >> 2) & 3));
+      const int cnt = (int)((cw >> (8 * (wl & 3))) & 0xffu);
       const int64_t lb = (rb0 + wr0 + wl) * CAP;
       float s2[NSC];
       int i2[NSC];
@@ -283,10 +298,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       a.lscore[lb + lane] = s2[0];
       a.lidx[lb + lane] = i2[0];
       const float t64 = rdlane(s2[0], 63);
-      if (lane == 0) {
-        s_thr[wr0 + wl] = t64;
-        s_cnt[wr0 + wl] = 64;
-      }
+      if (lane == 0) s_thr[wr0 + wl] = t64;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     WAVE_LDS_SYNC();
@@ -296,7 +308,10 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * gi + 4 * g + r;
         const bool done = row < 64 ? ((d0 >> row) & 1) : ((d1 >> (row - 64)) & 1);
-        if (done) nthr[gi][r] = -(s_thr[wr0 + row] * a.scaled);
+        if (done) {
+          nthr[gi][r] = -(s_thr[wr0 + row] * a.scaled);
+          cntp[gi] = (cntp[gi] & ~(0xffu << (8 * r))) | (64u << (8 * r));
+        }
       }
   };
 
@@ -350,9 +365,14 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup ends
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  for (int e = lane; e < 16 * G; e += 64) {  // each wave its own rows
-    const int64_t si = rb0 + wr0 + e;
-    if (si < a.n_src) a.lcnt[si] = s_cnt[wr0 + e];
+  if (i16 == 0) {
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t si = rb0 + wr0 + 16 * gi + 4 * g + r;
+        if (si < a.n_src) a.lcnt[si] = (int)((cntp[gi] >> (8 * r)) & 0xffu);
+      }
   }
   if (tid == 0 && a.scanned) atomicAdd(a.scanned, (unsigned long long)c);  // chunks this workgroup scanned
 }
