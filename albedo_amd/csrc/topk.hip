@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
   constexpr int NQ = C::NQ, NJ = C::NJ, RB = C::RB, CAP = TOPK_CAP;
   // a list is compacted to its best 64 once it holds more than TRIG (<= TRIG + 16 <= 64·NSC entries):
   // frequent enough that the threshold follows the running 64th best
-  constexpr int TRIG = TOPK_CAP - 16, NSC = TOPK_CAP / 64;
+  constexpr int TRIG = TOPK_TRIG, NSC = TOPK_CAP / 64;
   static_assert(TRIG + 16 <= 64 * NSC && TRIG + 16 <= CAP && TRIG + 16 <= 255, "compaction width, byte counters");
   extern __shared__ __attribute__((aligned(16))) char lds[];  // one LDS object (glds pipelining)
   float* s_thr = reinterpret_cast<float*>(lds + C::NSTG * C::SLOT);  // [RWG] thresholds (unscaled)

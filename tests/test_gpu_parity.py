@@ -511,12 +511,20 @@ def test_device_synthetic_generator_matches_numpy(gpu_lib):
     assert np.array_equal(u[:m], ref["user"]) and np.array_equal(i[:m], ref["item"])
 
 
-def _check_rows_fp64(gpu_lib, c, side, rows_ids, X_ids, X, Y_ids, Y, k):
+def _gram_fp64(Y, chunk=1 << 20):
+    """YᵀY in fp64, accumulated over row chunks (no fp64 copy of a 20M-row factor matrix)."""
+    G = np.zeros((Y.shape[1], Y.shape[1]))
+    for r0 in range(0, Y.shape[0], chunk):
+        Yc = Y[r0:r0 + chunk].astype(np.float64)
+        G += Yc.T @ Yc
+    return G
+
+
+def _check_rows_fp64(gpu_lib, c, side, rows_ids, X_ids, X, Y_ids, Y, k, gram=None):
     """Rows `rows_ids` of `side` (solved into X) equal the fp64 solve of Spark's implicit normal
     equation from the src factors Y, built from the engine's own CSR; returns the worst error."""
     from albedo_amd import _lib as L
-    Y64 = Y.astype(np.float64)
-    G = Y64.T @ Y64
+    G = _gram_fp64(Y) if gram is None else gram
     n_row = np.empty(1, np.int64)
     worst = 0.0
     for rid in rows_ids:
@@ -527,7 +535,7 @@ def _check_rows_fp64(gpu_lib, c, side, rows_ids, X_ids, X, Y_ids, Y, k):
         L.check(gpu_lib.als_get_row_ratings(c.h, side, int(rid), cap, L.ptr(src, C.c_int32), L.ptr(rat, C.c_float),
                                             L.ptr(n_row, C.c_int64)))
         n = int(n_row[0])
-        Yr = Y64[np.searchsorted(Y_ids, src[:n])]
+        Yr = Y[np.searchsorted(Y_ids, src[:n])].astype(np.float64)
         cvec = 40.0 * np.abs(rat[:n].astype(np.float64))
         A = G + (Yr.T * cvec) @ Yr + 0.5 * np.sum(rat[:n] > 0) * np.eye(k)
         b = Yr.T @ np.where(rat[:n] > 0, 1.0 + cvec, 0.0)
@@ -570,6 +578,42 @@ def test_c2_scale_rows_match_fp64_solve(gpu_lib):
     _, U = c.factors(0)
     rng = np.random.default_rng(0)
     _check_rows_fp64(gpu_lib, c, 0, uids[rng.choice(len(uids), 200, replace=False)], uids, U, iids, V, 64)
+
+
+def test_c4_scale_rows_match_fp64_solve(gpu_lib):
+    """Full-size property at BASELINE config 4 (20M x 4M, 1B stars, rank 128; the bench workload):
+    after an item and a user half-sweep from Spark-style init, the three most starred repos
+    (10^6+ stars: split-K builds), random repo and user rows equal the fp64 solution of Spark's
+    normal equation built on the host from the engine's own CSR (the Gram of the 20M user rows
+    accumulated in fp64 over row chunks)."""
+    from albedo_amd import _lib as L
+    from albedo_amd.synthetic import CONFIGS, popularity_table, user_degrees
+    spec = CONFIGS["c4"]
+    c = Ctx(gpu_lib, 128)
+    deg = user_degrees(spec)
+    prefix = np.ascontiguousarray(np.r_[0, np.cumsum(deg)].astype(np.int64))
+    del deg
+    cw, perm = popularity_table(spec)
+    L.check(gpu_lib.als_set_ratings_synthetic(c.h, spec.seed, spec.rounds, spec.n_users, spec.n_items,
+                                              L.ptr(prefix, C.c_int64), L.ptr(np.ascontiguousarray(cw), C.c_double),
+                                              L.ptr(np.ascontiguousarray(perm), C.c_int32)))
+    del prefix
+    assert gpu_lib.als_num_ratings(c.h) > 0.99 * spec.nnz
+    L.check(gpu_lib.als_init_factors(c.h))
+    uids, U0 = c.factors(0)
+    c.half(1)
+    iids, V = c.factors(1)
+    ideg = np.empty(iids.size, np.int64)
+    L.check(gpu_lib.als_get_degrees(c.h, 1, L.ptr(ideg, C.c_int64)))
+    top = iids[np.argsort(-ideg, kind="stable")[:3]]
+    assert ideg.max() > 1_000_000
+    rng = np.random.default_rng(4)
+    _check_rows_fp64(gpu_lib, c, 1, np.r_[top, rng.choice(iids, 30, replace=False)], iids, V, uids, U0, 128,
+                     gram=_gram_fp64(U0))
+    del U0
+    c.half(0)
+    _, U = c.factors(0)
+    _check_rows_fp64(gpu_lib, c, 0, uids[rng.choice(len(uids), 100, replace=False)], uids, U, iids, V, 128)
 
 
 # ---- NNLS (nonnegative = true) --------------------------------------------------------------
