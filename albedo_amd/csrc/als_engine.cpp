@@ -1314,7 +1314,7 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   const int CH = topk_chunk_rows(KP);
   const int64_t n_chunks = (T.n + CH - 1) / CH;
   DevBuf d_th, d_head, d_keys, d_perm, d_tmp, d_dstids;
-  if (!exact_only) {
+  {  // also for k > 64: the exact scan visits the dst rows in this norm order and stops early
     HIPCHK(d_th.ensure((size_t)n_chunks * CH * KP * 2));
     HIPCHK(d_head.ensure((size_t)n_chunks * 4));
     HIPCHK(d_keys.ensure((size_t)T.n * 8));

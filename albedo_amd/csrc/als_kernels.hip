@@ -261,7 +261,7 @@ hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64
 // Entries with c = 0 (implicit zero ratings) contribute nothing to A or b and are masked out.
 // =============================================================================================
 template <int KP, int D>
-__global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
+__global__ __launch_bounds__(256, (D == 16 && KP <= 128) ? 6 : 1) void solve_light_kernel(SolveArgs a) {
   constexpr int NB = D / 16, NT = NB * (NB + 1) / 2, LDK = D + 1, NHC = KP / 64;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
@@ -313,10 +313,13 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
     sdl[cc] = (cc < a.kreal && dd > 0.f) ? frsq(dd) : 0.f;
   }
   WAVE_LDS_SYNC();
-  if constexpr (D == 64) {
-    // S on split-fp16 MFMA (hi·hi + hi·lo + lo·hi, 32 columns per instruction: 120 instead of 320
-    // fp32 MFMAs).  One power-of-two scale for the whole row (so S unscales exactly):
-    // |Z[.][c]| < 2^(13 - e_c) (colscale), hence |z_c · sd_c| <= max_c sd_c · 2^(13 - e_c).
+  if constexpr (D == 64 || KEEPZ) {
+    // S on split-fp16 MFMA (hi·hi + hi·lo + lo·hi, 32 columns per instruction: at D = 64 120 instead
+    // of 320 fp32 MFMAs, at D = 16 12 x 16 cycles instead of 32 x 32).  One power-of-two scale for the
+    // whole row (so S unscales exactly): |Z[.][c]| < 2^(13 - e_c) (colscale), hence
+    // |z_c · sd_c| <= max_c sd_c · 2^(13 - e_c).  With the gathered rows in registers (KEEPZ) the
+    // 32-deep k-slots of block q take columns 16(2q) + 4g .. +3 and 16(2q+1) + 4g .. +3: both MFMA
+    // operands are Zs, so any column-to-slot assignment gives the same S.
     float bnd = 0.f;
 #pragma unroll
     for (int h = 0; h < NHC; ++h) {
@@ -330,12 +333,20 @@ __global__ __launch_bounds__(256) void solve_light_kernel(SolveArgs a) {
     constexpr int NQ = KP / 32;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const f32x4 s0 = ld4(sdl + 32 * q + 8 * g), s1 = ld4(sdl + 32 * q + 8 * g + 4);
+      const f32x4 s0 = KEEPZ ? ld4(sdl + 32 * q + 4 * g) : ld4(sdl + 32 * q + 8 * g);
+      const f32x4 s1 = KEEPZ ? ld4(sdl + 32 * q + 16 + 4 * g) : ld4(sdl + 32 * q + 8 * g + 4);
       f16x8 zh[NB], zl[NB];
 #pragma unroll
       for (int I = 0; I < NB; ++I) {
-        const float* zp = a.Z + (int64_t)colB[I] * KP + 32 * q + 8 * g;
-        const f32x4 v0 = vB[I] ? ld4(zp) : zero4(), v1 = vB[I] ? ld4(zp + 4) : zero4();
+        f32x4 v0, v1;
+        if constexpr (KEEPZ) {
+          v0 = zf[I][2 * q];
+          v1 = zf[I][2 * q + 1];
+        } else {
+          const float* zp = a.Z + (int64_t)colB[I] * KP + 32 * q + 8 * g;
+          v0 = vB[I] ? ld4(zp) : zero4();
+          v1 = vB[I] ? ld4(zp + 4) : zero4();
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float v = (e < 4 ? v0[e] * s0[e] : v1[e - 4] * s1[e - 4]) * sc;

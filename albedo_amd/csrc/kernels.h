@@ -120,7 +120,7 @@ struct TopkArgs {
 };
 constexpr int TOPK_KC = 64;     // candidates rescored exactly per src row (k <= 64)
 constexpr int TOPK_CAP = 128;   // candidate list capacity per src row (compacted to 64 above TOPK_TRIG)
-constexpr int TOPK_TRIG = 80;   // compaction trigger: frequent enough that thresholds follow the running 64th best
+constexpr int TOPK_TRIG = 112;  // compaction trigger: frequent enough that thresholds follow the running 64th best
 constexpr int TOPK_MAX = 512;   // k above TOPK_KC: exact full scan (topk_exact_kernel)
 int topk_chunk_rows(int KP);    // dst rows per scan chunk (Th / head are padded to whole chunks)
 size_t topk_sort_temp_bytes(int64_t n_dst);

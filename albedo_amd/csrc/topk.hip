@@ -567,13 +567,26 @@ __global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32
   for (int h = 0; h < 2 * P; ++h) { bs[h] = -INFINITY; bi[h] = -1; }
   int nin = 0;                // newcomer batches buffered (wave-uniform)
   float thr = -INFINITY;      // the kept list's last score once full
+  // with the prepared norm order (a.perm / a.head) dst rows are visited by descending norm and a wave
+  // stops once ‖s‖·‖t_j‖ bounds every later F2J score below its own 64·P-th best (which is <= the
+  // merged k-th): F2J(s, t) <= ‖s‖‖t‖(1 + (KP+2)·2^-24), covered by the 2^-14 factor
+  float snrm = 0.f;
+  if (a.perm) {
+    double nn = 0.0;
+    for (int c = lane; c < a.kreal; c += 64) nn += (double)s[c] * (double)s[c];
+    for (int o = 32; o > 0; o >>= 1) nn += __shfl_xor(nn, o);
+    snrm = __double2float_ru(sqrt(nn)) * 1.00006103515625f;
+  }
+  const int ch = topk_chunk_rows_dev<KP>();
   for (int64_t j0 = (int64_t)wave * 64; j0 < a.n_dst; j0 += 256) {
-    const int64_t dj = j0 + lane;
-    const float sc = dj < a.n_dst ? f2j_dot_v4(s, a.T + dj * KP, a.kreal) : -INFINITY;
+    if (a.perm && thr > -INFINITY && snrm * a.head[j0 / ch] < thr) break;
+    const int64_t pj = j0 + lane;
+    const int64_t dj = (a.perm && pj < a.n_dst) ? (int64_t)a.perm[pj] : pj;
+    const float sc = pj < a.n_dst ? f2j_dot_v4(s, a.T + dj * KP, a.kreal) : -INFINITY;
     if (!__any(sc >= thr)) continue;
     static_for<0, P>([&](auto hh) {
       constexpr int h = decltype(hh)::value;
-      if (nin == h) { bs[P + h] = sc; bi[P + h] = dj < a.n_dst ? (int)dj : -1; }
+      if (nin == h) { bs[P + h] = sc; bi[P + h] = pj < a.n_dst ? (int)dj : -1; }
     });
     if (++nin == P) {
       wave_bitonic<2 * P>(bs, bi);
