@@ -1439,7 +1439,8 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
       c->topk_stats[0] += nc;
       c->topk_stats[1] += (int64_t)flagged.size();
       c->topk_stats[2] += (int64_t)scanned;
-      c->topk_stats[3] += (nc + topk_rows_per_workgroup(KP, nc, c->n_cu) - 1) / topk_rows_per_workgroup(KP, nc, c->n_cu) * n_chunks;
+      c->topk_stats[3] += (nc + topk_rows_per_workgroup(KP, nc, c->n_cu) - 1) / topk_rows_per_workgroup(KP, nc, c->n_cu) *
+                          4 * n_chunks * CH;  // dst rows x waves
       if (!flagged.empty()) {
         HIPCHK(d_flag.ensure(flagged.size() * 4));
         HIPCHK(hipMemcpy(d_flag.p, flagged.data(), flagged.size() * 4, hipMemcpyHostToDevice));

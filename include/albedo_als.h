@@ -159,8 +159,8 @@ int als_path_stats(const als_ctx* ctx, int dst_side, int64_t* out4);
 int als_solver_stats(const als_ctx* ctx, int dst_side, int64_t* out4);
 /* Top-k counters since als_create (als_recommend with k <= 64): out[0] = src rows through the MFMA
  * scan, out[1] = rows whose candidate set failed certification and were re-scored by the exact scan,
- * out[2] = dst chunks scanned (summed over scan workgroups), out[3] = chunks a scan without the
- * norm-order early exit would take. */
+ * out[2] = dst rows scanned (summed over the scan waves), out[3] = the same without the norm-order
+ * early exit. */
 int als_topk_stats(const als_ctx* ctx, int64_t* out4);
 /* Synchronise the context's streams (bench barrier helper). */
 int als_synchronize(als_ctx* ctx);
