@@ -261,11 +261,13 @@ hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64
 // Entries with c = 0 (implicit zero ratings) contribute nothing to A or b and are masked out.
 // =============================================================================================
 template <int KP, int D>
-__global__ __launch_bounds__(256, (D == 16 && KP <= 128) ? 6 : 1) void solve_light_kernel(SolveArgs a) {
-  constexpr int NB = D / 16, NT = NB * (NB + 1) / 2, LDK = D + 1, NHC = KP / 64;
+__global__ __launch_bounds__(256, (D == 16 && KP <= 128) ? 6 : (D == 64 && KP == 128) ? 4 : 1) void solve_light_kernel(SolveArgs a) {
+  // K and L live in LDS as packed lower triangles (element (r, c), c <= r, at r(r+1)/2 + c): half the
+  // LDS of a full D x D image, so four D = 64 workgroups fit a CU instead of two
+  constexpr int NB = D / 16, NT = NB * (NB + 1) / 2, TRI = D * (D + 1) / 2 + 64, NHC = KP / 64;  // + 64: sink
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
-  float* Ks = smem + wave * D * LDK;
+  float* Ks = smem + wave * TRI;
   const int64_t ridx = (int64_t)blockIdx.x * 4 + wave;
   if (ridx >= a.n_rows) return;  // wave-uniform; this kernel has no workgroup barrier
   const int j = a.rows[ridx];
@@ -303,7 +305,7 @@ __global__ __launch_bounds__(256, (D == 16 && KP <= 128) ? 6 : 1) void solve_lig
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = zero4();
   // D^-1/2 of the row, one rsq per column (lane c, c+64, ...) into this wave's LDS slot
-  float* sdl = smem + 4 * D * LDK + wave * KP;
+  float* sdl = smem + 4 * TRI + wave * KP;
   bool bad = false;
 #pragma unroll
   for (int h = 0; h < NHC; ++h) {
@@ -393,9 +395,8 @@ __global__ __launch_bounds__(256, (D == 16 && KP <= 128) ? 6 : 1) void solve_lig
     constexpr TilePair p = upper_tile(decltype(t)::value, NB);
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
-      const int row = 16 * p.a + 4 * g + rr, cl = 16 * p.b + i16;
-      Ks[row * LDK + cl] = acc[t][rr];
-      Ks[cl * LDK + row] = acc[t][rr];
+      const int row = 16 * p.a + 4 * g + rr, cl = 16 * p.b + i16;  // p.a <= p.b: cl >= row off the diagonal
+      Ks[(p.a < p.b || cl >= row) ? cl * (cl + 1) / 2 + row : TRI - 64 + lane] = acc[t][rr];  // else: sink
     }
   });
   WAVE_LDS_SYNC();
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(256, (D == 16 && KP <= 128) ? 6 : 1) void solve_lig
   float kr[D];
 #pragma unroll
   for (int m = 0; m < D; ++m) {
-    const float v = Ks[me * LDK + m];
+    const float v = Ks[me * (me + 1) / 2 + m];  // in bounds for m > me too (unused entries)
     kr[m] = (m == me) ? (valid ? v + cinv : 1.0f) : (valid ? v : 0.0f);
   }
   // Cholesky K = L Lᵀ, lane i holds row i (entries m <= i are L[i][m] when done); then the forward
@@ -456,12 +457,12 @@ __global__ __launch_bounds__(256, (D == 16 && KP <= 128) ? 6 : 1) void solve_lig
   WAVE_LDS_SYNC();
   if (lane < D) {
 #pragma unroll
-    for (int m = 0; m < D; ++m) Ks[lane * LDK + m] = kr[m];
+    for (int m = 0; m < D; ++m) Ks[m <= lane ? lane * (lane + 1) / 2 + m : TRI - 64 + lane] = kr[m];
   }
   WAVE_LDS_SYNC();
   float lt[D];
 #pragma unroll
-  for (int m = 0; m < D; ++m) lt[m] = Ks[m * LDK + me];
+  for (int m = 0; m < D; ++m) lt[m] = Ks[m * (m + 1) / 2 + me];  // L[m][me] (m >= me used)
   // backward: Lᵀ v = y
   if constexpr (D == 16) {
     static_for<0, D>([&](auto cc) {
@@ -536,7 +537,7 @@ hipError_t launch_solve_light(int KP, int D, const SolveArgs& a0, hipStream_t s)
   }
   const SolveArgs& a = a0;
   const int blocks = (int)((a.n_rows + 3) / 4);
-  const size_t lds = ((size_t)4 * D * (D + 1) + (size_t)4 * KP) * sizeof(float);  // K per wave + D^-1/2
+  const size_t lds = ((size_t)4 * (D * (D + 1) / 2 + 64) + (size_t)4 * KP) * sizeof(float);  // K per wave + D^-1/2
 #define LIGHT(kp, dd) \
   if (KP == kp && D == dd) { solve_light_kernel<kp, dd><<<blocks, 256, lds, s>>>(a); return hipGetLastError(); }
   LIGHT(64, 16) LIGHT(64, 32) LIGHT(64, 64) LIGHT(128, 16) LIGHT(128, 32) LIGHT(128, 64)
