@@ -55,15 +55,47 @@ def synthetic_starring(users=20000, repos=4000, stars=400000, seed=42):
             "starring": d["rating"].astype(np.float64)}
 
 
+SYNTH_SIDECAR = "_albedo_synth.json"  # Hadoop-hidden: parquet readers skip it
+
+
 def load_raw_starring(users=20000, repos=4000, stars=400000, seed=42, path=None):
     """DatasetUtils.loadRawStarringDS (:111-123): loadOrCreateDataFrame(dataDir/today/
-    rawStarringDF.parquet, <read app_repostarring + starring = 1.0>) -- the parquet cache is read
+    rawStarringDF.parquet, <read app_repostarring + starring = 1.0>) -- the parquet data is read
     when present, else the synthetic stand-in is written there first.  `path=False` skips the
-    cache (pure in-memory)."""
+    cache (pure in-memory).
+
+    Like the reference's date-keyed cache, an existing dataset wins over the requested sizes.  The
+    synthetic spec is kept beside the parquet parts (`_albedo_synth.json`, hidden from readers), and
+    a cache hit whose spec differs from the request -- or a dataset this code did not write -- is
+    reported on stderr with the row count actually used."""
     if path is False:
         return synthetic_starring(users, repos, stars, seed)
-    return persistence.load_or_create_dataframe(path or settings.raw_starring_path(),
-                                                lambda: synthetic_starring(users, repos, stars, seed))
+    import json
+    import sys
+    path = path or settings.raw_starring_path()
+    spec = {"users": int(users), "repos": int(repos), "stars": int(stars), "seed": int(seed)}
+    created = []
+
+    def create():
+        created.append(True)
+        return synthetic_starring(users, repos, stars, seed)
+
+    df = persistence.load_or_create_dataframe(path, create)
+    side = os.path.join(path, SYNTH_SIDECAR)
+    if created:
+        if os.path.isdir(path):
+            with open(side, "w") as fh:
+                json.dump(spec, fh)
+        return df
+    cached = None
+    if os.path.exists(side):
+        with open(side) as fh:
+            cached = json.load(fh)
+    if cached != spec:
+        what = f"synthetic spec {cached}" if cached else "a dataset not written by this builder"
+        print(f"[albedo] {path}: using the existing starring data ({df['user_id'].size} rows, {what}) instead of "
+              f"the requested {spec}; delete the directory to regenerate", file=sys.stderr)
+    return df
 
 
 def sample_test_users(stars, seed, n=250):

@@ -170,6 +170,15 @@ int set_device(als_ctx* c) {
   return ALS_OK;
 }
 
+// world > 1: the factor-chunk gathers of the last half-sweep run on st2 behind the solve.  Anything
+// that rewrites factor buffers with default-stream copies, or returns to the caller as "done",
+// first waits for both streams.
+int drain(als_ctx* c) {
+  if (c->st2) HIPCHK(hipStreamSynchronize(c->st2));
+  if (c->st) HIPCHK(hipStreamSynchronize(c->st));
+  return ALS_OK;
+}
+
 int validate(const als_params* p) {
   auto bad = [](const char* name, double v) {
     char buf[160];
@@ -294,6 +303,7 @@ bool use_wave_kernel(const als_ctx* c);
 // (the light limit follows KP), factor and rotated-factor buffers, Gram slabs.  Called after ingest
 // and again by als_set_params, so several fits (a CV grid) share one ingest.
 int rank_layout(als_ctx* c) {
+  TRYC(drain(c));
   const int64_t lmax = light_limit(c);
   c->split_len = split_chunk_len();
   for (int side = 0; side < 2; ++side) {
@@ -509,6 +519,7 @@ int ingest_device(als_ctx* c, int64_t n, const int32_t* d_user, const int32_t* d
 
 // upload host factors (dense order, [n][rank]) for this rank's own rows
 int upload_factors(als_ctx* c, int side, const float* f, int64_t ld) {
+  TRYC(drain(c));
   Side& S = c->s[side];
   std::vector<float> h((size_t)std::max<int64_t>(S.own_n, 1) * c->KP, 0.f);
   for (int64_t r = 0; r < S.own_n; ++r)
@@ -1003,8 +1014,8 @@ void als_destroy(als_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->dev);
   if (c->st) (void)hipStreamSynchronize(c->st);
+  if (c->st2) (void)hipStreamSynchronize(c->st2);  // no RCCL gather may be in flight at the destroy
   if (c->comm) (void)ncclCommDestroy(c->comm);
-  if (c->st2) (void)hipStreamSynchronize(c->st2);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->evc)
@@ -1115,6 +1126,7 @@ int als_init_factors_random(als_ctx* c, uint64_t seed) {
   if (!c) return fail(ALS_E_INVALID_ARGUMENT, "null context");
   if (!c->has_ratings) return fail(ALS_E_STATE, "set ratings first");
   TRYC(set_device(c));
+  TRYC(drain(c));
   for (int side = 0; side < 2; ++side) {
     Side& S = c->s[side];
     HIPCHK(launch_init_random(c->KP, c->p.rank, S.d_X.as<float>(), S.own_n, seed + 0x51ED270B27u * (side + 1),
@@ -1556,8 +1568,7 @@ int als_topk_stats(const als_ctx* c, int64_t* out4) {
 int als_synchronize(als_ctx* c) {
   if (!c) return fail(ALS_E_INVALID_ARGUMENT, "null context");
   TRYC(set_device(c));
-  HIPCHK(hipStreamSynchronize(c->st));
-  return ALS_OK;
+  return drain(c);  // both streams: the bench barrier covers the trailing factor gathers
 }
 
 int als_synth_generate(int32_t device, uint64_t seed, int32_t rounds, int64_t n_users, int64_t n_items,

@@ -179,13 +179,28 @@ def write_starring(path: str, stars: dict, rows_per_part: int = 1 << 24) -> None
     _finish(path)
 
 
+def _data_files(path: str):
+    """Parquet data files of a dataset directory, as Spark's reader lists them: every non-hidden
+    file (Hadoop hidden = `_*` / `.*`) ending in `.parquet`, in name order -- Spark's
+    `part-NNNNN-<uuid>-c000.snappy.parquet` as well as a pandas/pyarrow export (`<uuid>-0.parquet`)."""
+    names = sorted(n for n in os.listdir(path) if not n.startswith(("_", ".")))
+    files = [os.path.join(path, n) for n in names if n.endswith(".parquet") and os.path.isfile(os.path.join(path, n))]
+    if not files and any(os.path.isdir(os.path.join(path, n)) for n in names):
+        raise ValueError(f"{path}: partitioned parquet directories (column=value/ subdirectories) are not supported; "
+                         "write the starring rows as one flat parquet directory")
+    return files
+
+
 def read_starring(path: str, columns=STARRING_COLUMNS) -> dict:
     """`spark.read.parquet(path)` of a Starring dataset: dict of numpy columns (timestamps as
-    datetime64[us]); a missing path raises FileNotFoundError ("Path does not exist")."""
+    datetime64[us]).  A missing path raises FileNotFoundError ("Path does not exist"); an existing
+    directory without parquet data files raises ValueError (nothing is ever deleted here)."""
     import pyarrow.parquet as pq
-    parts = _parts(path) if os.path.isdir(path) else ([path] if os.path.isfile(path) else [])
-    if not parts:
+    if not os.path.exists(path):
         raise FileNotFoundError(f"Path does not exist: {path}")
+    parts = _data_files(path) if os.path.isdir(path) else [path]
+    if not parts:
+        raise ValueError(f"Unable to infer schema for Parquet: {path} holds no parquet data files")
     cols = {c: [] for c in columns}
     for f in parts:
         t = pq.read_table(f, columns=list(columns))
@@ -196,11 +211,12 @@ def read_starring(path: str, columns=STARRING_COLUMNS) -> dict:
 
 
 def load_or_create_dataframe(path: str, create_fn) -> dict:
-    """DatasetUtils.loadOrCreateDataFrame: read the parquet cache at `path`, or create the data,
-    write it there (mode overwrite) and return it."""
-    try:
+    """DatasetUtils.loadOrCreateDataFrame (DatasetUtils.scala:36-50): read the parquet data at
+    `path`; only when the path does not exist ("Path does not exist") create the data, write it there
+    and return it.  Any other read error of an existing path propagates: a user's directory is never
+    replaced."""
+    if os.path.exists(path):
         return read_starring(path)
-    except FileNotFoundError:
-        df = create_fn()
-        write_starring(path, df)
-        return df
+    df = create_fn()
+    write_starring(path, df)
+    return df

@@ -119,3 +119,41 @@ def test_builder_reads_starring_cache(tmp_path):
     act1 = into_user_items(s1["user_id"], s1["repo_id"], s1["starred_at"], 30)
     act2 = into_user_items(s2["user_id"], s2["repo_id"], s2["starred_at"], 30)
     assert act1 == act2
+
+
+def test_existing_starring_dir_is_read_never_replaced(tmp_path, capsys):
+    """an existing --starring-path is data, not a cache miss.  A pandas/pyarrow
+    export (`<uuid>-0.parquet`) is read as is; a directory without parquet files raises and keeps
+    its contents; only a path that does not exist is created (DatasetUtils.scala:36-50)."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from albedo_amd import builder
+    d = tmp_path / "export"
+    d.mkdir()
+    t = pa.table({"user_id": pa.array([7, 8], pa.int32()), "repo_id": pa.array([1, 2], pa.int32()),
+                  "starred_at": pa.array(np.array([1500000000, 1500000001], "datetime64[s]").astype("datetime64[us]")),
+                  "starring": pa.array([1.0, 1.0])})
+    pq.write_table(t, str(d / "1f2e3d4c-0.parquet"))
+    (d / "_SUCCESS").write_text("")
+    got = P.load_or_create_dataframe(str(d), lambda: pytest.fail("existing data must not be recreated"))
+    assert got["user_id"].tolist() == [7, 8]
+    s = builder.load_raw_starring(100, 10, 500, seed=1, path=str(d))
+    assert s["user_id"].tolist() == [7, 8]
+    assert "not written by this builder" in capsys.readouterr().err
+    bad = tmp_path / "notes"
+    bad.mkdir()
+    (bad / "README.txt").write_text("keep me")
+    with pytest.raises(ValueError):
+        P.load_or_create_dataframe(str(bad), lambda: pytest.fail("must not create over an existing directory"))
+    assert (bad / "README.txt").read_text() == "keep me"
+
+
+def test_builder_cache_reports_spec_mismatch(tmp_path, capsys):
+    from albedo_amd import builder
+    path = str(tmp_path / "stars.parquet")
+    builder.load_raw_starring(300, 60, 2000, seed=3, path=path)
+    assert capsys.readouterr().err == ""
+    builder.load_raw_starring(300, 60, 2000, seed=3, path=path)
+    assert capsys.readouterr().err == ""
+    builder.load_raw_starring(400, 60, 2000, seed=3, path=path)
+    assert "using the existing starring data" in capsys.readouterr().err
