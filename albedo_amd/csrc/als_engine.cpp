@@ -155,6 +155,7 @@ struct als_ctx {
   // top-k counters, cumulative: [0] rows through the MFMA scan, [1] rows re-scored by the exact scan
   // (certification misses), [2] dst chunks scanned, [3] dst chunks a full scan would take
   int64_t topk_stats[4] = {0, 0, 0, 0};
+  std::vector<int32_t> last_rescan;  // src ids the last als_recommend sent to the exact rescan
   int split_len = 0;             // ratings per split-K chunk (0: no split)
   std::vector<float> h_P32, h_lam32, h_Gt;  // host staging of async H2D copies (outlive the sync)
   int slab_blocks = 0;
@@ -1255,6 +1256,18 @@ int als_model_create(int32_t rank, int64_t nu, const int32_t* uids, const float*
   return ALS_OK;
 }
 
+// top-k experiment switches, read once: ALBEDO_TOPK_DRAIN=1 (wait for every DMA each chunk),
+// ALBEDO_TOPK_ORDER=0 (no scan order / starting thresholds), ALBEDO_TOPK_THR0=0 (order only)
+struct TopkKnobs {
+  int drain = 0;
+  bool order = true, thr0 = true;
+  TopkKnobs() {
+    if (const char* e = std::getenv("ALBEDO_TOPK_DRAIN")) drain = std::atoi(e);
+    if (const char* e = std::getenv("ALBEDO_TOPK_ORDER")) order = std::atoi(e) != 0;
+    if (const char* e = std::getenv("ALBEDO_TOPK_THR0")) thr0 = std::atoi(e) != 0;
+  }
+};
+
 int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_t n_subset, int32_t* src_ids_out,
                   int32_t* dst_ids_out, float* scores_out) {
   if (!c || (side != 0 && side != 1) || !dst_ids_out || !scores_out)
@@ -1264,6 +1277,7 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
     return fail(ALS_E_UNSUPPORTED, "num above " + std::to_string(TOPK_MAX) + " is not supported by this engine");
   const bool exact_only = k > TOPK_KC;  // no MFMA pre-selection: exact full scan of every row
   TRYC(set_device(c));
+  static const TopkKnobs tk;
   const int src = side, dst = 1 - side;
   TRYC(materialize(c, src));
   TRYC(materialize(c, dst));
@@ -1299,6 +1313,7 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
       std::fill(scores_out + i * k, scores_out + (i + 1) * k, NAN);
     }
   const bool dense_out = (int64_t)known.size() == nq;  // results land in place, no scatter
+  c->last_rescan.clear();
   if (known.empty() || T.n == 0) return ALS_OK;
   // max row norms (error bound of the pre-selection; fp16 split scales), on the device
   double tmax = 0.0, smax = 0.0;
@@ -1386,9 +1401,8 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
       // scan order: rows that stop at similar depths share a workgroup (topk_order); the select
       // writes each row's results back to its own slot
       TopkArgs b = a;
-      if (const char* de = std::getenv("ALBEDO_TOPK_DRAIN")) b.drain = std::atoi(de);
-      const char* oe = std::getenv("ALBEDO_TOPK_ORDER");
-      if (!(oe && std::atoi(oe) == 0)) {
+      b.drain = tk.drain;
+      if (tk.order) {
         HIPCHK(d_okeys.ensure(nc * 8));
         HIPCHK(d_order.ensure(nc * 8));
         HIPCHK(d_srcs.ensure(nc * 4));
@@ -1400,52 +1414,18 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
         b.src_rows = d_srcs.as<int32_t>();
         b.out_pos = d_order.as<uint32_t>();
         b.thr0 = d_thr.as<float>() + nc;
-        if (const char* te = std::getenv("ALBEDO_TOPK_THR0"); te && std::atoi(te) == 0) b.thr0 = nullptr;
+        if (!tk.thr0) b.thr0 = nullptr;
       }
       HIPCHK(launch_topk(KP, b, c->n_cu, c->st));
-      if (const char* dbg = std::getenv("ALBEDO_TOPK_DEBUG"); dbg && std::atoi(dbg) > 0) {  // diagnostics
-        std::vector<int32_t> lc(nc), nd(nc);
-        std::vector<float> t0(nc);
-        std::vector<uint32_t> od(nc);
-        HIPCHK(hipStreamSynchronize(c->st));
-        HIPCHK(hipMemcpy(lc.data(), d_lc.p, nc * 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(nd.data(), d_need.p, nc * 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(t0.data(), d_thr.as<float>() + nc, nc * 4, hipMemcpyDeviceToHost));
-        if (b.out_pos) HIPCHK(hipMemcpy(od.data(), b.out_pos, nc * 4, hipMemcpyDeviceToHost));
-        int64_t lt64 = 0, nflag = 0, printed = 0;
-        for (int64_t i = 0; i < nc; ++i) {
-          const int64_t o = b.out_pos ? od[i] : i;
-          lt64 += lc[i] < 64;
-          nflag += nd[o] != 0;
-          bool bad = false;
-          if (lc[i] >= 64 && std::getenv("ALBEDO_TOPK_THR0")) {  // thr0 above the scan's own 64th best?
-            std::vector<float> ls(std::min(lc[i], TOPK_CAP));
-            HIPCHK(hipMemcpy(ls.data(), d_ls.as<float>() + i * TOPK_CAP, ls.size() * 4, hipMemcpyDeviceToHost));
-            std::nth_element(ls.begin(), ls.begin() + 63, ls.end(), std::greater<float>());
-            bad = t0[i] > ls[63];
-            if (bad && printed < 8) std::fprintf(stderr, "[topk dbg] pos %lld thr0 %.9g above the scan's 64th %.9g\n",
-                                                 (long long)i, t0[i], ls[63]);
-            lt64 += bad;
-          }
-          if ((nd[o] || bad) && printed < 8) {
-            std::vector<float> ls(std::min(lc[i], TOPK_CAP));
-            HIPCHK(hipMemcpy(ls.data(), d_ls.as<float>() + i * TOPK_CAP, ls.size() * 4, hipMemcpyDeviceToHost));
-            std::sort(ls.begin(), ls.end(), std::greater<float>());
-            std::fprintf(stderr, "[topk dbg] pos %lld (slot %lld) cnt %d thr0 %.9g best %.9g 64th %.9g\n", (long long)i,
-                         (long long)o, lc[i], b.thr0 ? t0[i] : 0.f, ls.empty() ? 0.f : ls[0],
-                         ls.size() >= 64 ? ls[63] : -1.f);
-            ++printed;
-          }
-        }
-        std::fprintf(stderr, "[topk dbg] rows %lld, lists < 64: %lld, flagged %lld\n", (long long)nc, (long long)lt64,
-                     (long long)nflag);
-      }
       std::vector<int32_t> need(nc);
       HIPCHK(hipMemcpyAsync(need.data(), d_need.p, nc * 4, hipMemcpyDeviceToHost, c->st));
       HIPCHK(hipStreamSynchronize(c->st));
       std::vector<int32_t> flagged;
       for (int64_t i = 0; i < nc; ++i)
-        if (need[i]) flagged.push_back((int32_t)i);
+        if (need[i]) {
+          flagged.push_back((int32_t)i);
+          c->last_rescan.push_back(S.ids[known[q0 + i]]);
+        }
       unsigned long long scanned = 0;
       HIPCHK(hipMemcpy(&scanned, d_scan.p, 8, hipMemcpyDeviceToHost));
       c->topk_stats[0] += nc;
@@ -1562,6 +1542,13 @@ int als_solver_stats(const als_ctx* c, int dst_side, int64_t* out4) {
 int als_topk_stats(const als_ctx* c, int64_t* out4) {
   if (!c || !out4) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
   for (int i = 0; i < 4; ++i) out4[i] = c->topk_stats[i];
+  return ALS_OK;
+}
+
+int als_topk_last_rescan(const als_ctx* c, int32_t* src_ids_out, int64_t cap, int64_t* n_out) {
+  if (!c || !n_out) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  *n_out = (int64_t)c->last_rescan.size();
+  if (src_ids_out && *n_out <= cap) std::memcpy(src_ids_out, c->last_rescan.data(), c->last_rescan.size() * 4);
   return ALS_OK;
 }
 

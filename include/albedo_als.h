@@ -162,6 +162,10 @@ int als_solver_stats(const als_ctx* ctx, int dst_side, int64_t* out4);
  * out[2] = dst rows scanned (summed over the scan waves), out[3] = the same without the norm-order
  * early exit. */
 int als_topk_stats(const als_ctx* ctx, int64_t* out4);
+/* The src ids whose candidate set failed certification in the last als_recommend call (k <= 64) and
+ * were re-scored by the exact scan, in output order; *n_out = their count, ids filled when
+ * n_out <= cap.  Parity tests check exactly these rows against the oracle. */
+int als_topk_last_rescan(const als_ctx* ctx, int32_t* src_ids_out, int64_t cap, int64_t* n_out);
 /* Synchronise the context's streams (bench barrier helper). */
 int als_synchronize(als_ctx* ctx);
 

@@ -24,6 +24,8 @@ def load():
         _lib.oracle_gram.restype = C.c_int
         _lib.oracle_gram.argtypes = [C.c_int64, C.c_int, P, P, C.c_int]
         _lib.oracle_max_threads.restype = C.c_int
+        _lib.oracle_recommend.restype = C.c_int
+        _lib.oracle_recommend.argtypes = [C.c_int64, P, C.c_int64, P, P, C.c_int, C.c_int, P, P, C.c_int]
     return _lib
 
 
@@ -74,3 +76,22 @@ def solve_rows(Ysrc, G, ptr, col, val, *, reg, alpha, implicit=True, threads=Non
     if rc != 0:
         raise ValueError(f"oracle solve_rows: row {rc - 1} not positive definite (rc={rc})")
     return X
+
+
+def recommend(src_f, dst_ids, dst_f, num, threads=None):
+    """oracle/spark_als.py:recommend_for_all in C/OpenMP (F2J sdot, (score desc, id asc) top-num):
+    (ids[n_src, num], scores[n_src, num]), -1 / NaN padded."""
+    lib = load()
+    dst_ids = np.asarray(dst_ids, dtype=np.int32)
+    order = np.argsort(dst_ids, kind="stable")
+    ids_sorted = np.ascontiguousarray(dst_ids[order])
+    dst_f = np.ascontiguousarray(np.asarray(dst_f, dtype=np.float32)[order])
+    src_f = np.ascontiguousarray(src_f, dtype=np.float32)
+    n_src, k = src_f.shape
+    out_i = np.empty((n_src, num), np.int32)
+    out_s = np.empty((n_src, num), np.float32)
+    rc = lib.oracle_recommend(n_src, _p(src_f), len(ids_sorted), _p(ids_sorted), _p(dst_f), k, num, _p(out_i),
+                              _p(out_s), threads or lib.oracle_max_threads())
+    if rc != 0:
+        raise ValueError(f"oracle_recommend failed (rc={rc}): duplicate dst ids?")
+    return out_i, out_s

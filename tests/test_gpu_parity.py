@@ -546,76 +546,6 @@ def _check_rows_fp64(gpu_lib, c, side, rows_ids, X_ids, X, Y_ids, Y, k, gram=Non
     return worst
 
 
-def test_c2_scale_rows_match_fp64_solve(gpu_lib):
-    """Full-size property at BASELINE config 2 (1M x 200k, 50M nnz, rank 64): after an item and a
-    user half-sweep from Spark-style init, sampled rows of every degree bucket -- and the 10 most
-    starred repos (the power-law tail, 10^5 stars) -- equal the fp64 solution of Spark's normal
-    equation built on the host from the engine's own inputs."""
-    from albedo_amd import _lib as L
-    from albedo_amd.synthetic import CONFIGS, popularity_table, user_degrees
-    spec = CONFIGS["c2"]
-    c = Ctx(gpu_lib, 64)
-    deg = user_degrees(spec)
-    prefix = np.ascontiguousarray(np.r_[0, np.cumsum(deg)].astype(np.int64))
-    cw, perm = popularity_table(spec)
-    L.check(gpu_lib.als_set_ratings_synthetic(c.h, spec.seed, spec.rounds, spec.n_users, spec.n_items,
-                                              L.ptr(prefix, C.c_int64), L.ptr(np.ascontiguousarray(cw), C.c_double),
-                                              L.ptr(np.ascontiguousarray(perm), C.c_int32)))
-    assert gpu_lib.als_num_ratings(c.h) > 0.99 * spec.nnz
-    L.check(gpu_lib.als_init_factors(c.h))
-    uids, U0 = c.factors(0)
-    c.half(1)
-    iids, V = c.factors(1)
-    deg = np.empty(iids.size, np.int64)
-    L.check(gpu_lib.als_get_degrees(c.h, 1, L.ptr(deg, C.c_int64)))
-    top = iids[np.argsort(-deg, kind="stable")[:10]]
-    assert deg.max() > 100_000  # the tail this arm is about
-    rng = np.random.default_rng(1)
-    _check_rows_fp64(gpu_lib, c, 1, np.r_[top, rng.choice(iids, 100, replace=False)], iids, V, uids, U0, 64)
-    c.half(0)
-    st = c.stats(0)
-    assert st[0] > 0 and st[2] > 0  # both solve paths ran
-    _, U = c.factors(0)
-    rng = np.random.default_rng(0)
-    _check_rows_fp64(gpu_lib, c, 0, uids[rng.choice(len(uids), 200, replace=False)], uids, U, iids, V, 64)
-
-
-def test_c4_scale_rows_match_fp64_solve(gpu_lib):
-    """Full-size property at BASELINE config 4 (20M x 4M, 1B stars, rank 128; the bench workload):
-    after an item and a user half-sweep from Spark-style init, the three most starred repos
-    (10^6+ stars: split-K builds), random repo and user rows equal the fp64 solution of Spark's
-    normal equation built on the host from the engine's own CSR (the Gram of the 20M user rows
-    accumulated in fp64 over row chunks)."""
-    from albedo_amd import _lib as L
-    from albedo_amd.synthetic import CONFIGS, popularity_table, user_degrees
-    spec = CONFIGS["c4"]
-    c = Ctx(gpu_lib, 128)
-    deg = user_degrees(spec)
-    prefix = np.ascontiguousarray(np.r_[0, np.cumsum(deg)].astype(np.int64))
-    del deg
-    cw, perm = popularity_table(spec)
-    L.check(gpu_lib.als_set_ratings_synthetic(c.h, spec.seed, spec.rounds, spec.n_users, spec.n_items,
-                                              L.ptr(prefix, C.c_int64), L.ptr(np.ascontiguousarray(cw), C.c_double),
-                                              L.ptr(np.ascontiguousarray(perm), C.c_int32)))
-    del prefix
-    assert gpu_lib.als_num_ratings(c.h) > 0.99 * spec.nnz
-    L.check(gpu_lib.als_init_factors(c.h))
-    uids, U0 = c.factors(0)
-    c.half(1)
-    iids, V = c.factors(1)
-    ideg = np.empty(iids.size, np.int64)
-    L.check(gpu_lib.als_get_degrees(c.h, 1, L.ptr(ideg, C.c_int64)))
-    top = iids[np.argsort(-ideg, kind="stable")[:3]]
-    assert ideg.max() > 1_000_000
-    rng = np.random.default_rng(4)
-    _check_rows_fp64(gpu_lib, c, 1, np.r_[top, rng.choice(iids, 30, replace=False)], iids, V, uids, U0, 128,
-                     gram=_gram_fp64(U0))
-    del U0
-    c.half(0)
-    _, U = c.factors(0)
-    _check_rows_fp64(gpu_lib, c, 0, uids[rng.choice(len(uids), 100, replace=False)], uids, U, iids, V, 128)
-
-
 # ---- NNLS (nonnegative = true) --------------------------------------------------------------
 
 def test_golden_f5_nnls_half_sweep_and_fit(gpu_lib):
