@@ -246,6 +246,24 @@ int allgather_rows(als_ctx* c, float* buf, int64_t rows_per_rank, hipStream_t s)
   return ALS_OK;
 }
 
+// all-gather of host blocks: buf holds world blocks of n floats (this rank's filled); bytes are
+// moved, never combined (ids travel as float bit patterns)
+int allgather_host(als_ctx* c, float* buf, int64_t n) {
+  if (c->world == 1) return ALS_OK;
+  if (c->comm) {
+    DevBuf d;
+    HIPCHK(d.ensure((size_t)n * c->world * 4));
+    float* dp = d.as<float>();
+    HIPCHK(hipMemcpyAsync(dp + (int64_t)c->rank * n, buf + (int64_t)c->rank * n, n * 4, hipMemcpyHostToDevice, c->st));
+    NCCLCHK(ncclAllGather(dp + (int64_t)c->rank * n, dp, n, ncclFloat, c->comm, c->st));
+    HIPCHK(hipMemcpyAsync(buf, dp, (size_t)n * c->world * 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return ALS_OK;
+  }
+  if (c->h_allgather(c->h_user, buf, n) != 0) return fail(ALS_E_RCCL, "host all-gather callback failed");
+  return ALS_OK;
+}
+
 // Gathers layout chunks [q0, q1) of the own rows `own` ([nch·chpad][KP], zero past own_n) into
 // `full` ([prows][KP]) on stream s: chunk q of every rank is one contiguous all-gather.
 int gather_chunks(als_ctx* c, const Side& S, const float* own, float* full, int q0, int q1, hipStream_t s) {
@@ -1354,10 +1372,16 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   HIPCHK(d_dstids.ensure(T.n * 4));
   HIPCHK(hipMemcpyAsync(d_dstids.p, T.ids.data(), T.n * 4, hipMemcpyHostToDevice, c->st));
   const int64_t chunk = 1 << 20;
+  // world > 1 (SURVEY §8(e) "Top-k: shard users"): rank r scores the r-th contiguous slice of the
+  // known src rows against the replicated dst factors; the lists are all-gathered afterwards
+  const int64_t n_known = (int64_t)known.size();
+  const int64_t per_rank = (n_known + c->world - 1) / c->world;
+  const int64_t lo = std::min<int64_t>(n_known, (int64_t)c->rank * per_rank);
+  const int64_t hi = std::min<int64_t>(n_known, lo + per_rank);
   DevBuf d_src, d_ls, d_li, d_lc, d_oid, d_osc, d_need, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp, d_thr;
   HIPCHK(d_scan.ensure(8));
-  for (int64_t q0 = 0; q0 < (int64_t)known.size(); q0 += chunk) {
-    const int64_t nc = std::min<int64_t>(chunk, (int64_t)known.size() - q0);
+  for (int64_t q0 = lo; q0 < hi; q0 += chunk) {
+    const int64_t nc = std::min<int64_t>(chunk, hi - q0);
     HIPCHK(d_src.ensure(nc * 4));
     HIPCHK(d_oid.ensure(nc * k * 4));
     HIPCHK(d_osc.ensure(nc * k * 4));
@@ -1452,6 +1476,24 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
       for (int64_t i = 0; i < nc; ++i) {
         std::memcpy(dst_ids_out + pos[q0 + i] * k, &oid[i * k], k * 4);
         std::memcpy(scores_out + pos[q0 + i] * k, &osc[i * k], k * 4);
+      }
+    }
+  }
+  if (c->world > 1 && per_rank > 0) {  // every rank ends with every list: one all-gather of the slices
+    std::vector<float> blk((size_t)c->world * per_rank * k * 2, 0.f);
+    float* mine = blk.data() + (size_t)c->rank * per_rank * k * 2;
+    for (int64_t i = lo; i < hi; ++i) {
+      std::memcpy(mine + (size_t)(i - lo) * k * 2, dst_ids_out + pos[i] * k, k * 4);
+      std::memcpy(mine + (size_t)(i - lo) * k * 2 + k, scores_out + pos[i] * k, k * 4);
+    }
+    TRYC(allgather_host(c, blk.data(), per_rank * k * 2));
+    for (int r = 0; r < c->world; ++r) {
+      if (r == c->rank) continue;
+      const int64_t rl = std::min<int64_t>(n_known, (int64_t)r * per_rank), rh = std::min<int64_t>(n_known, rl + per_rank);
+      const float* b = blk.data() + (size_t)r * per_rank * k * 2;
+      for (int64_t i = rl; i < rh; ++i) {
+        std::memcpy(dst_ids_out + pos[i] * k, b + (size_t)(i - rl) * k * 2, k * 4);
+        std::memcpy(scores_out + pos[i] * k, b + (size_t)(i - rl) * k * 2 + k, k * 4);
       }
     }
   }

@@ -66,6 +66,18 @@ def main():
             f = np.empty((n, k), np.float32)
             L.check(lib.als_get_factors(h, side, None, L.ptr(f, C.c_float)))
             res[name] = f
+        # recommendForAllUsers(10), users sharded across the ranks, lists all-gathered
+        n_u = lib.als_num_rows(h, 0)
+        ids = np.empty((n_u, 10), np.int32)
+        sc = np.empty((n_u, 10), np.float32)
+        L.check(lib.als_recommend(h, 0, 10, None, n_u, None, L.ptr(ids, C.c_int32), L.ptr(sc, C.c_float)))
+        st = np.zeros(4, np.int64)
+        L.check(lib.als_topk_stats(h, L.ptr(st, C.c_int64)))
+        assert 0 < st[0] < n_u, f"rank {rank} scored {st[0]} of {n_u} users: not sharded"
+        res["topk_ids"], res["topk_sc"] = ids, sc
+        if rank != 0:  # every rank holds every list
+            np.save(out + f".rank{rank}.npy", ids)
+        res["split_rows"] = np.array([lib.als_num_rows(h, 1)])
         lib.als_destroy(h)
     else:
         from oracle import cbind

@@ -19,12 +19,12 @@ def _free_port():
     return p
 
 
-def _launch(mode, out, world=2, timeout=300):
+def _launch(mode, out, world=2, timeout=300, env_extra=None):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port))
+                   MASTER_PORT=str(port), **(env_extra or {}))
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_worker.py"), mode, out],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     outs = []
@@ -62,14 +62,28 @@ def test_sharded_layout_cpu(tmp_path, world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,nonneg", [(2, False), (3, False), (3, True)])
-def test_sharded_fit_gpu_matches_single(gpu_lib, tmp_path, world, nonneg):
+@pytest.mark.parametrize("world,nonneg,split", [(2, False, 0), (3, False, 0), (3, True, 0), (2, False, 128),
+                                                (3, False, 128), (3, True, 128)])
+def test_sharded_fit_gpu_matches_single(gpu_lib, tmp_path, world, nonneg, split):
     """Ranks sharing the box's GPU run the engine's sharded fit (device remap into the chunk-major
     gathered layout, the solve in row chunks whose factors are gathered on a second stream, host
     transport for the Gram all-reduce and the all-gathers); factors match the single-process oracle.
-    nonneg: the NNLS half-sweeps (lockstep + per-row kernels) with the blocking chunk gathers."""
-    res = _launch("gpunn" if nonneg else "gpu", str(tmp_path / "gpu.npz"), world=world)
+    nonneg: the NNLS half-sweeps (lockstep + per-row kernels) with the blocking chunk gathers.
+    split: ALBEDO_SPLIT_CHUNK=128 sends every row above 128 ratings (the popular repos) through the
+    split-K partial + reduce path inside the solve chunks of each rank.  Then recommendForAllUsers(10)
+    with the users sharded across the ranks: every rank returns every list, bit-exact against the
+    oracle scorer on the fitted factors."""
+    env = {"ALBEDO_SPLIT_CHUNK": str(split)} if split else None
+    out = str(tmp_path / "gpu.npz")
+    res = _launch("gpunn" if nonneg else "gpu", out, world=world, env_extra=env)
     B, U0, V0 = _problem()
+    if split:
+        assert np.max(np.diff(B.i_ptr)) > 2 * split  # rows that really take the split-K path
     U, V = O.fit(B, rank=16, max_iter=3, reg=0.5, alpha=40.0, init_user=U0, init_item=V0, nonnegative=nonneg)
     rel = lambda a, b: np.max(np.abs(a - b)) / np.max(np.abs(b))
     assert rel(res["U"], U) < 1e-3 and rel(res["V"], V) < 1e-3
+    ref_ids, ref_sc = O.recommend_for_all(B.user_ids, res["U"], B.item_ids, res["V"], 10)
+    assert np.array_equal(res["topk_ids"], ref_ids)
+    assert np.array_equal(res["topk_sc"].view(np.uint32), ref_sc.view(np.uint32))
+    for r in range(1, world):
+        assert np.array_equal(np.load(out + f".rank{r}.npy"), ref_ids)

@@ -1,0 +1,23 @@
+#!/bin/bash
+# One GPU call of this round: steps given as arguments are run in order, each under its own time
+# limit; the call stops at the first failing step.  usage: tools/gpu_call.sh <step> [<step> ...]
+#   bounds_c2 | bounds_c4 | tests_scale | tests_all | smoke | bench_c4 | bench_c2 | bench_c5
+set -e
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+PYT="python -u -m pytest -x -v --timeout 600 --timeout-method thread"
+for s in "$@"; do
+  echo "== $s $(date +%T)"
+  case $s in
+    bounds_c2) timeout -k 10 300 python -u tools/topk_bounds.py --config c2 --sweeps 10 --sample 16384 --out gpurun_out/bounds_c2_s10.json > gpurun_out/bounds_c2.log 2>&1 ;;
+    bounds_c4) timeout -k 10 500 python -u tools/topk_bounds.py --config c4 --sweeps 25 --sample 16384 --out gpurun_out/bounds_c4_s25.json > gpurun_out/bounds_c4.log 2>&1 ;;
+    tests_scale) timeout -k 10 900 $PYT tests/test_gpu_scale.py -s > gpurun_out/tests_scale.log 2>&1 ;;
+    tests_all) timeout -k 10 1100 $PYT tests -m gpu > gpurun_out/tests_all.log 2>&1 ;;
+    smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke.log 2>&1 ;;
+    bench_c4) timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_c4.json 2> gpurun_out/bench_c4.err ;;
+    bench_c2) timeout -k 10 300 python -u bench.py --config c2 --steps 10 --warmup 5 > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.err ;;
+    bench_c5) timeout -k 10 400 python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo all-ok
