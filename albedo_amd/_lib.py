@@ -99,6 +99,7 @@ SIGNATURES = [
     ("als_model_create", C.c_int, [C.c_int32, C.c_int64, I32P, F32P, C.c_int64, I32P, F32P, C.c_int32, C.POINTER(P)]),
     ("als_recommend", C.c_int, [P, C.c_int, C.c_int32, I32P, C.c_int64, I32P, I32P, F32P]),
     ("als_predict", C.c_int, [P, C.c_int64, I32P, I32P, F32P]),
+    ("als_evaluate_ndcg", C.c_int, [P, C.c_int32, C.c_int64, I32P, I32P, I64P, F64P, I64P, I32P, F64P, C.c_int64]),
     ("als_last_timings", C.c_int, [P, C.c_int, F64P, C.c_int]),
     ("als_path_stats", C.c_int, [P, C.c_int, I64P]),
     ("als_solver_stats", C.c_int, [P, C.c_int, I64P]),

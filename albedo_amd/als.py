@@ -354,6 +354,34 @@ class ALSModel(_Params):
         return self._rec_frame(*self._recommend(_lib.ALS_ITEM, numUsers, items), self._p["itemCol"],
                                self._p["userCol"])
 
+    # ---- RankingEvaluator on the device (RankingEvaluator.scala:83-139) ----------------------------
+    def evaluate_ndcg(self, users, items, keys, k=30, per_user=False):
+        """NDCG@k of this model's top-k recommendations against intoUserActualItems(users, items,
+        keys desc, k), computed on the device (als_evaluate_ndcg): the albedo protocol of
+        ALSRecommenderBuilder.scala:92-104 without the lists leaving HBM.  Returns the mean, or
+        (mean, user ids, per-user values) with per_user=True."""
+        lib = load()
+        u = np.ascontiguousarray(_checked_cast(users, self._p["userCol"]))
+        it = np.ascontiguousarray(_checked_cast(items, self._p["itemCol"]))
+        ky = np.asarray(keys)
+        if ky.dtype.kind == "M":  # starred_at timestamps
+            ky = ky.astype("datetime64[us]").astype(np.int64)
+        ky = np.ascontiguousarray(ky, dtype=np.int64)
+        if not (u.size == it.size == ky.size):
+            raise ValueError("users, items and keys must have the same length")
+        mean = C.c_double()
+        nu = C.c_int64()
+        cap = int(np.unique(u).size) if per_user else 0
+        uo = np.empty(max(cap, 1), np.int32)
+        vo = np.empty(max(cap, 1), np.float64)
+        check(lib.als_evaluate_ndcg(self._h, int(k), u.size, ptr(u, C.c_int32), ptr(it, C.c_int32),
+                                    ptr(ky, C.c_int64), C.byref(mean), C.byref(nu),
+                                    ptr(uo, C.c_int32) if per_user else None,
+                                    ptr(vo, C.c_double) if per_user else None, cap))
+        if per_user:
+            return mean.value, uo[:nu.value], vo[:nu.value]
+        return mean.value
+
     # ---- persistence (Spark 2.2 ALSModelWriter / ALSModelReader layout: albedo_amd/persistence.py) ----
     MODEL_PARAMS = ("userCol", "itemCol", "predictionCol", "coldStartStrategy")  # ALSModelParams
 

@@ -1286,6 +1286,159 @@ struct TopkKnobs {
   }
 };
 
+// One recommendForAll* call's prepared dst side (topk.hip): max row norms (the pre-selection's error
+// bound), fp16 power-of-two scales, the descending-norm fp16 image with chunk head norms, dst ids on
+// the device; plus the per-chunk scratch reused by every src chunk.
+struct TopkPlan {
+  int src = 0, k = 0;
+  bool exact_only = false;
+  double tmax = 0.0, smax = 0.0, ssc = 1.0, tsc = 1.0;
+  int CH = 0;
+  int64_t n_chunks = 0;
+  DevBuf d_th, d_head, d_keys, d_perm, d_tmp, d_dstids;
+  DevBuf d_src, d_ls, d_li, d_lc, d_need, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp, d_thr;
+};
+
+int topk_plan(als_ctx* c, int src, int k, TopkPlan& P) {
+  P.src = src;
+  P.k = k;
+  P.exact_only = k > TOPK_KC;  // no MFMA pre-selection: exact full scan of every row
+  TRYC(materialize(c, src));
+  TRYC(materialize(c, 1 - src));
+  Side& S = c->s[src];
+  Side& T = c->s[1 - src];
+  const int KP = c->KP;
+  {
+    DevBuf d_nrm;
+    HIPCHK(d_nrm.ensure(16));
+    HIPCHK(launch_rownorm_max(T.d_orig.as<float>(), T.n, KP, c->p.rank, d_nrm.as<unsigned long long>(), c->st));
+    HIPCHK(launch_rownorm_max(S.d_orig.as<float>(), S.n, KP, c->p.rank, d_nrm.as<unsigned long long>() + 1, c->st));
+    double nr[2];
+    HIPCHK(hipMemcpyAsync(nr, d_nrm.p, 16, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    P.tmax = nr[0];
+    P.smax = nr[1];
+  }
+  // |entry| <= row norm, so scaling by 2^(13 - ceil(log2 max norm)) keeps every fp16 value < 2^13
+  auto pow2_scale = [](double m) {
+    if (!(m > 0.0) || !std::isfinite(m)) return 1.0;
+    int e = 0;
+    std::frexp(m, &e);  // m < 2^e
+    e = std::max(-60, std::min(60, 13 - e));
+    return std::ldexp(1.0, e);
+  };
+  P.ssc = pow2_scale(P.smax);
+  P.tsc = pow2_scale(P.tmax);
+  // dst side in descending-norm order, fp16 rows + chunk head norms (also for k > 64: the exact scan
+  // visits the dst rows in this norm order and stops early)
+  P.CH = topk_chunk_rows(KP);
+  P.n_chunks = (T.n + P.CH - 1) / P.CH;
+  HIPCHK(P.d_th.ensure((size_t)std::max<int64_t>(P.n_chunks, 1) * P.CH * KP * 2));
+  HIPCHK(P.d_head.ensure((size_t)std::max<int64_t>(P.n_chunks, 1) * 4));
+  HIPCHK(P.d_keys.ensure((size_t)std::max<int64_t>(T.n, 1) * 8));
+  HIPCHK(P.d_perm.ensure((size_t)std::max<int64_t>(T.n, 1) * 8));
+  const size_t tb = topk_sort_temp_bytes(T.n);
+  HIPCHK(P.d_tmp.ensure(std::max<size_t>(tb, 16)));
+  if (T.n > 0)
+    HIPCHK(topk_prepare(KP, c->p.rank, T.d_orig.as<float>(), T.n, (float)P.tsc, P.d_tmp.p, tb, P.d_keys.as<uint32_t>(),
+                        P.d_perm.as<uint32_t>(), P.d_th.p, P.d_head.as<float>(), c->st));
+  HIPCHK(P.d_dstids.ensure(std::max<int64_t>(T.n, 1) * 4));
+  HIPCHK(hipMemcpyAsync(P.d_dstids.p, T.ids.data(), T.n * 4, hipMemcpyHostToDevice, c->st));
+  HIPCHK(P.d_scan.ensure(8));
+  return ALS_OK;
+}
+
+// Top-k of the nc src rows `rows` (host, dense row indices) into the device lists d_oid / d_osc
+// ([nc][k], score desc, id asc); rows that fail certification are re-scored exactly and their ids
+// appended to c->last_rescan.  Enqueued on c->st; returns after the rescans are enqueued.
+int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int32_t* d_oid, float* d_osc) {
+  static const TopkKnobs tk;
+  Side& S = c->s[P.src];
+  Side& T = c->s[1 - P.src];
+  const int KP = c->KP, k = P.k;
+  if (nc <= 0) return ALS_OK;
+  HIPCHK(P.d_src.ensure(nc * 4));
+  HIPCHK(P.d_need.ensure(nc * 4));
+  if (!P.exact_only) {
+    HIPCHK(P.d_ls.ensure(nc * TOPK_CAP * 4));
+    HIPCHK(P.d_li.ensure(nc * TOPK_CAP * 4));
+    HIPCHK(P.d_lc.ensure(nc * 4));
+  }
+  HIPCHK(hipMemcpyAsync(P.d_src.p, rows, nc * 4, hipMemcpyHostToDevice, c->st));
+  HIPCHK(hipMemsetAsync(P.d_need.p, 0, nc * 4, c->st));
+  HIPCHK(hipMemsetAsync(P.d_scan.p, 0, 8, c->st));
+  TopkArgs a{};
+  a.S = S.d_orig.as<float>();
+  a.T = T.d_orig.as<float>();
+  a.src_rows = P.d_src.as<int32_t>();
+  a.n_src = nc;
+  a.n_dst = T.n;
+  a.dst_ids = P.d_dstids.as<int32_t>();
+  a.kreal = c->p.rank;
+  a.k = k;
+  a.tmax_norm = (float)(P.tmax * (1.0 + 1e-6));
+  a.Th = P.d_th.p;
+  a.head = P.d_head.as<float>();
+  a.perm = P.d_perm.as<uint32_t>();
+  a.n_chunks = P.n_chunks;
+  a.ssc = (float)P.ssc;
+  a.tsc = (float)P.tsc;
+  a.unscale = (float)(1.0 / (P.ssc * P.tsc));
+  a.scaled = (float)(P.ssc * P.tsc);
+  a.lscore = P.d_ls.as<float>();
+  a.lidx = P.d_li.as<int32_t>();
+  a.lcnt = P.d_lc.as<int32_t>();
+  a.out_ids = d_oid;
+  a.out_scores = d_osc;
+  a.need_exact = P.d_need.as<int32_t>();
+  a.scanned = P.d_scan.as<unsigned long long>();
+  if (P.exact_only) {
+    HIPCHK(launch_topk_exact(KP, a, nullptr, nc, c->st));
+    return ALS_OK;
+  }
+  // scan order: rows that stop at similar depths share a workgroup (topk_order); the select writes
+  // each row's results back to its own slot
+  TopkArgs b = a;
+  b.drain = tk.drain;
+  if (tk.order) {
+    HIPCHK(P.d_okeys.ensure(nc * 8));
+    HIPCHK(P.d_order.ensure(nc * 8));
+    HIPCHK(P.d_srcs.ensure(nc * 4));
+    const size_t otb = topk_order_temp_bytes(nc);
+    HIPCHK(P.d_otmp.ensure(std::max<size_t>(otb, 16)));
+    HIPCHK(P.d_thr.ensure(nc * 8));
+    HIPCHK(topk_order(KP, a, P.d_otmp.p, otb, P.d_okeys.as<uint32_t>(), P.d_order.as<uint32_t>(),
+                      P.d_srcs.as<int32_t>(), P.d_thr.as<float>(), P.d_thr.as<float>() + nc, c->st));
+    b.src_rows = P.d_srcs.as<int32_t>();
+    b.out_pos = P.d_order.as<uint32_t>();
+    b.thr0 = tk.thr0 ? P.d_thr.as<float>() + nc : nullptr;
+  }
+  HIPCHK(launch_topk(KP, b, c->n_cu, c->st));
+  std::vector<int32_t> need(nc);
+  unsigned long long scanned = 0;
+  HIPCHK(hipMemcpyAsync(need.data(), P.d_need.p, nc * 4, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipMemcpyAsync(&scanned, P.d_scan.p, 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  std::vector<int32_t> flagged;
+  for (int64_t i = 0; i < nc; ++i)
+    if (need[i]) {
+      flagged.push_back((int32_t)i);
+      c->last_rescan.push_back(S.ids[rows[i]]);
+    }
+  c->topk_stats[0] += nc;
+  c->topk_stats[1] += (int64_t)flagged.size();
+  c->topk_stats[2] += (int64_t)scanned;
+  const int rpw = topk_rows_per_workgroup(KP, nc, c->n_cu);
+  c->topk_stats[3] += (nc + rpw - 1) / rpw * 4 * P.n_chunks * P.CH;  // dst rows x waves
+  if (!flagged.empty()) {
+    HIPCHK(P.d_flag.ensure(flagged.size() * 4));
+    HIPCHK(hipMemcpyAsync(P.d_flag.p, flagged.data(), flagged.size() * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(launch_topk_exact(KP, a, P.d_flag.as<int32_t>(), (int64_t)flagged.size(), c->st));
+    HIPCHK(hipStreamSynchronize(c->st));  // flagged (host) must outlive the async copy
+  }
+  return ALS_OK;
+}
+
 int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_t n_subset, int32_t* src_ids_out,
                   int32_t* dst_ids_out, float* scores_out) {
   if (!c || (side != 0 && side != 1) || !dst_ids_out || !scores_out)
@@ -1293,15 +1446,11 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   if (k <= 0) return fail(ALS_E_INVALID_ARGUMENT, "num must be positive");
   if (k > TOPK_MAX)
     return fail(ALS_E_UNSUPPORTED, "num above " + std::to_string(TOPK_MAX) + " is not supported by this engine");
-  const bool exact_only = k > TOPK_KC;  // no MFMA pre-selection: exact full scan of every row
   TRYC(set_device(c));
-  static const TopkKnobs tk;
-  const int src = side, dst = 1 - side;
+  const int src = side;
   TRYC(materialize(c, src));
-  TRYC(materialize(c, dst));
   Side& S = c->s[src];
-  Side& T = c->s[dst];
-  const int KP = c->KP;
+  const Side& T = c->s[1 - src];
   const int64_t nq = subset ? n_subset : S.n;
   // id -> row: a merge walk when the subset is ascending (the usual case), binary search otherwise
   std::vector<int32_t> qrow(nq);
@@ -1333,44 +1482,8 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   const bool dense_out = (int64_t)known.size() == nq;  // results land in place, no scatter
   c->last_rescan.clear();
   if (known.empty() || T.n == 0) return ALS_OK;
-  // max row norms (error bound of the pre-selection; fp16 split scales), on the device
-  double tmax = 0.0, smax = 0.0;
-  {
-    DevBuf d_nrm;
-    HIPCHK(d_nrm.ensure(16));
-    HIPCHK(launch_rownorm_max(T.d_orig.as<float>(), T.n, KP, c->p.rank, d_nrm.as<unsigned long long>(), c->st));
-    HIPCHK(launch_rownorm_max(S.d_orig.as<float>(), S.n, KP, c->p.rank, d_nrm.as<unsigned long long>() + 1, c->st));
-    double nr[2];
-    HIPCHK(hipMemcpyAsync(nr, d_nrm.p, 16, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
-    tmax = nr[0];
-    smax = nr[1];
-  }
-  // |entry| <= row norm, so scaling by 2^(13 - ceil(log2 max norm)) keeps every fp16 value < 2^13
-  auto pow2_scale = [](double m) {
-    if (!(m > 0.0) || !std::isfinite(m)) return 1.0;
-    int e = 0;
-    std::frexp(m, &e);  // m < 2^e
-    e = std::max(-60, std::min(60, 13 - e));
-    return std::ldexp(1.0, e);
-  };
-  const double ssc = pow2_scale(smax), tsc = pow2_scale(tmax);
-  // dst side in descending-norm order, fp16 rows + chunk head norms (topk.hip)
-  const int CH = topk_chunk_rows(KP);
-  const int64_t n_chunks = (T.n + CH - 1) / CH;
-  DevBuf d_th, d_head, d_keys, d_perm, d_tmp, d_dstids;
-  {  // also for k > 64: the exact scan visits the dst rows in this norm order and stops early
-    HIPCHK(d_th.ensure((size_t)n_chunks * CH * KP * 2));
-    HIPCHK(d_head.ensure((size_t)n_chunks * 4));
-    HIPCHK(d_keys.ensure((size_t)T.n * 8));
-    HIPCHK(d_perm.ensure((size_t)T.n * 8));
-    const size_t tb = topk_sort_temp_bytes(T.n);
-    HIPCHK(d_tmp.ensure(std::max<size_t>(tb, 16)));
-    HIPCHK(topk_prepare(KP, c->p.rank, T.d_orig.as<float>(), T.n, (float)tsc, d_tmp.p, tb, d_keys.as<uint32_t>(),
-                        d_perm.as<uint32_t>(), d_th.p, d_head.as<float>(), c->st));
-  }
-  HIPCHK(d_dstids.ensure(T.n * 4));
-  HIPCHK(hipMemcpyAsync(d_dstids.p, T.ids.data(), T.n * 4, hipMemcpyHostToDevice, c->st));
+  TopkPlan P;
+  TRYC(topk_plan(c, src, k, P));
   const int64_t chunk = 1 << 20;
   // world > 1 (SURVEY §8(e) "Top-k: shard users"): rank r scores the r-th contiguous slice of the
   // known src rows against the replicated dst factors; the lists are all-gathered afterwards
@@ -1378,91 +1491,12 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   const int64_t per_rank = (n_known + c->world - 1) / c->world;
   const int64_t lo = std::min<int64_t>(n_known, (int64_t)c->rank * per_rank);
   const int64_t hi = std::min<int64_t>(n_known, lo + per_rank);
-  DevBuf d_src, d_ls, d_li, d_lc, d_oid, d_osc, d_need, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp, d_thr;
-  HIPCHK(d_scan.ensure(8));
+  DevBuf d_oid, d_osc;
   for (int64_t q0 = lo; q0 < hi; q0 += chunk) {
     const int64_t nc = std::min<int64_t>(chunk, hi - q0);
-    HIPCHK(d_src.ensure(nc * 4));
     HIPCHK(d_oid.ensure(nc * k * 4));
     HIPCHK(d_osc.ensure(nc * k * 4));
-    HIPCHK(d_need.ensure(nc * 4));
-    if (!exact_only) {
-      HIPCHK(d_ls.ensure(nc * TOPK_CAP * 4));
-      HIPCHK(d_li.ensure(nc * TOPK_CAP * 4));
-      HIPCHK(d_lc.ensure(nc * 4));
-    }
-    HIPCHK(hipMemcpyAsync(d_src.p, known.data() + q0, nc * 4, hipMemcpyHostToDevice, c->st));
-    HIPCHK(hipMemsetAsync(d_need.p, 0, nc * 4, c->st));
-    HIPCHK(hipMemsetAsync(d_scan.p, 0, 8, c->st));
-    TopkArgs a{};
-    a.S = S.d_orig.as<float>();
-    a.T = T.d_orig.as<float>();
-    a.src_rows = d_src.as<int32_t>();
-    a.n_src = nc;
-    a.n_dst = T.n;
-    a.dst_ids = d_dstids.as<int32_t>();
-    a.kreal = c->p.rank;
-    a.k = k;
-    a.tmax_norm = (float)(tmax * (1.0 + 1e-6));
-    a.Th = d_th.p;
-    a.head = d_head.as<float>();
-    a.perm = d_perm.as<uint32_t>();
-    a.n_chunks = n_chunks;
-    a.ssc = (float)ssc;
-    a.tsc = (float)tsc;
-    a.unscale = (float)(1.0 / (ssc * tsc));
-    a.scaled = (float)(ssc * tsc);
-    a.lscore = d_ls.as<float>();
-    a.lidx = d_li.as<int32_t>();
-    a.lcnt = d_lc.as<int32_t>();
-    a.out_ids = d_oid.as<int32_t>();
-    a.out_scores = d_osc.as<float>();
-    a.need_exact = d_need.as<int32_t>();
-    a.scanned = d_scan.as<unsigned long long>();
-    if (exact_only) {
-      HIPCHK(launch_topk_exact(KP, a, nullptr, nc, c->st));
-    } else {
-      // scan order: rows that stop at similar depths share a workgroup (topk_order); the select
-      // writes each row's results back to its own slot
-      TopkArgs b = a;
-      b.drain = tk.drain;
-      if (tk.order) {
-        HIPCHK(d_okeys.ensure(nc * 8));
-        HIPCHK(d_order.ensure(nc * 8));
-        HIPCHK(d_srcs.ensure(nc * 4));
-        const size_t otb = topk_order_temp_bytes(nc);
-        HIPCHK(d_otmp.ensure(std::max<size_t>(otb, 16)));
-        HIPCHK(d_thr.ensure(nc * 8));
-        HIPCHK(topk_order(KP, a, d_otmp.p, otb, d_okeys.as<uint32_t>(), d_order.as<uint32_t>(), d_srcs.as<int32_t>(),
-                          d_thr.as<float>(), d_thr.as<float>() + nc, c->st));
-        b.src_rows = d_srcs.as<int32_t>();
-        b.out_pos = d_order.as<uint32_t>();
-        b.thr0 = d_thr.as<float>() + nc;
-        if (!tk.thr0) b.thr0 = nullptr;
-      }
-      HIPCHK(launch_topk(KP, b, c->n_cu, c->st));
-      std::vector<int32_t> need(nc);
-      HIPCHK(hipMemcpyAsync(need.data(), d_need.p, nc * 4, hipMemcpyDeviceToHost, c->st));
-      HIPCHK(hipStreamSynchronize(c->st));
-      std::vector<int32_t> flagged;
-      for (int64_t i = 0; i < nc; ++i)
-        if (need[i]) {
-          flagged.push_back((int32_t)i);
-          c->last_rescan.push_back(S.ids[known[q0 + i]]);
-        }
-      unsigned long long scanned = 0;
-      HIPCHK(hipMemcpy(&scanned, d_scan.p, 8, hipMemcpyDeviceToHost));
-      c->topk_stats[0] += nc;
-      c->topk_stats[1] += (int64_t)flagged.size();
-      c->topk_stats[2] += (int64_t)scanned;
-      c->topk_stats[3] += (nc + topk_rows_per_workgroup(KP, nc, c->n_cu) - 1) / topk_rows_per_workgroup(KP, nc, c->n_cu) *
-                          4 * n_chunks * CH;  // dst rows x waves
-      if (!flagged.empty()) {
-        HIPCHK(d_flag.ensure(flagged.size() * 4));
-        HIPCHK(hipMemcpy(d_flag.p, flagged.data(), flagged.size() * 4, hipMemcpyHostToDevice));
-        HIPCHK(launch_topk_exact(KP, a, d_flag.as<int32_t>(), (int64_t)flagged.size(), c->st));
-      }
-    }
+    TRYC(topk_run_rows(c, P, known.data() + q0, nc, d_oid.as<int32_t>(), d_osc.as<float>()));
     if (dense_out) {
       HIPCHK(hipMemcpyAsync(dst_ids_out + q0 * k, d_oid.p, nc * k * 4, hipMemcpyDeviceToHost, c->st));
       HIPCHK(hipMemcpyAsync(scores_out + q0 * k, d_osc.p, nc * k * 4, hipMemcpyDeviceToHost, c->st));
@@ -1490,12 +1524,97 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
     for (int r = 0; r < c->world; ++r) {
       if (r == c->rank) continue;
       const int64_t rl = std::min<int64_t>(n_known, (int64_t)r * per_rank), rh = std::min<int64_t>(n_known, rl + per_rank);
-      const float* b = blk.data() + (size_t)r * per_rank * k * 2;
+      const float* bb = blk.data() + (size_t)r * per_rank * k * 2;
       for (int64_t i = rl; i < rh; ++i) {
-        std::memcpy(dst_ids_out + pos[i] * k, b + (size_t)(i - rl) * k * 2, k * 4);
-        std::memcpy(scores_out + pos[i] * k, b + (size_t)(i - rl) * k * 2 + k, k * 4);
+        std::memcpy(dst_ids_out + pos[i] * k, bb + (size_t)(i - rl) * k * 2, k * 4);
+        std::memcpy(scores_out + pos[i] * k, bb + (size_t)(i - rl) * k * 2 + k, k * 4);
       }
     }
+  }
+  return ALS_OK;
+}
+
+int als_evaluate_ndcg(als_ctx* c, int32_t k, int64_t n, const int32_t* user, const int32_t* item, const int64_t* key,
+                      double* ndcg_out, int64_t* n_users_out, int32_t* users_out, double* per_user_out, int64_t cap) {
+  if (!c || !ndcg_out || !n_users_out || (n > 0 && (!user || !item || !key)))
+    return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  if (k <= 0) return fail(ALS_E_INVALID_ARGUMENT, "ranking position k should be positive");
+  if (k > TOPK_KC) return fail(ALS_E_UNSUPPORTED, "NDCG@k on the device supports k <= " + std::to_string(TOPK_KC));
+  TRYC(set_device(c));
+  TRYC(materialize(c, ALS_USER));
+  Side& S = c->s[ALS_USER];
+  *ndcg_out = NAN;
+  *n_users_out = 0;
+  c->last_rescan.clear();
+  if (n <= 0 || S.n == 0) return ALS_OK;
+  hipStream_t st = c->st;
+  // 1. intoUserActualItems on the device: group by model user (inner join), top-k by (key desc, item asc)
+  DevBuf d_user, d_item, d_key, d_ids, d_row, d_rows, d_idx, d_idxs, d_runs, d_cnt, d_off, d_nr, d_tmp;
+  HIPCHK(d_user.ensure(n * 4));
+  HIPCHK(d_item.ensure(n * 4));
+  HIPCHK(d_key.ensure(n * 8));
+  HIPCHK(d_ids.ensure(S.n * 4));
+  HIPCHK(hipMemcpyAsync(d_user.p, user, n * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_item.p, item, n * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_key.p, key, n * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_ids.p, S.ids.data(), S.n * 4, hipMemcpyHostToDevice, st));
+  for (DevBuf* b : {&d_row, &d_rows, &d_idx, &d_idxs, &d_runs, &d_cnt}) HIPCHK(b->ensure(n * 4));
+  HIPCHK(d_off.ensure(n * 8));
+  HIPCHK(d_nr.ensure(8));
+  const size_t tb = eval_sort_temp_bytes(n);
+  HIPCHK(d_tmp.ensure(std::max<size_t>(tb, 16)));
+  HIPCHK(eval_group_users(d_user.as<int32_t>(), n, d_ids.as<int32_t>(), S.n, d_tmp.p, tb, d_row.as<uint32_t>(),
+                          d_rows.as<uint32_t>(), d_idx.as<uint32_t>(), d_idxs.as<uint32_t>(), d_runs.as<uint32_t>(),
+                          d_cnt.as<int32_t>(), d_off.as<int64_t>(), d_nr.as<int64_t>(), st));
+  int64_t nr = 0;
+  HIPCHK(hipMemcpyAsync(&nr, d_nr.p, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  std::vector<int32_t> rows(nr);
+  HIPCHK(hipMemcpyAsync(rows.data(), d_runs.p, nr * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (nr > 0 && (uint32_t)rows[nr - 1] == 0xFFFFFFFFu) --nr;  // ids unknown to the model: dropped
+  rows.resize(nr);
+  *n_users_out = nr;
+  if (nr == 0) return ALS_OK;
+  DevBuf d_act, d_actn, d_gain, d_vals;
+  HIPCHK(d_act.ensure(nr * k * 4));
+  HIPCHK(d_actn.ensure(nr * 4));
+  HIPCHK(eval_actual_lists(d_idxs.as<uint32_t>(), d_off.as<int64_t>(), d_cnt.as<int32_t>(), nr, d_key.as<int64_t>(),
+                           d_item.as<int32_t>(), k, d_act.as<int32_t>(), d_actn.as<int32_t>(), st));
+  // ndcgAt's gains from the host's libm: the host evaluator's table (1.0 / math.log(i + 2))
+  std::vector<double> gain(k);
+  for (int i = 0; i < k; ++i) gain[i] = 1.0 / std::log((double)(i + 2));
+  HIPCHK(d_gain.ensure(k * 8));
+  HIPCHK(hipMemcpyAsync(d_gain.p, gain.data(), k * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(d_vals.ensure(nr * 8));
+  // 2. intoUserPredictedItems: the users' top-k lists stay on the device; 3. ndcgAt per user
+  TopkPlan P;
+  TRYC(topk_plan(c, ALS_USER, k, P));
+  const int64_t per_rank = (nr + c->world - 1) / c->world;
+  const int64_t lo = std::min<int64_t>(nr, (int64_t)c->rank * per_rank), hi = std::min<int64_t>(nr, lo + per_rank);
+  const int64_t chunk = 1 << 20;
+  DevBuf d_oid, d_osc;
+  for (int64_t q0 = lo; q0 < hi; q0 += chunk) {
+    const int64_t nc = std::min<int64_t>(chunk, hi - q0);
+    HIPCHK(d_oid.ensure(nc * k * 4));
+    HIPCHK(d_osc.ensure(nc * k * 4));
+    TRYC(topk_run_rows(c, P, rows.data() + q0, nc, d_oid.as<int32_t>(), d_osc.as<float>()));
+    HIPCHK(eval_ndcg(d_oid.as<int32_t>(), d_act.as<int32_t>() + q0 * k, d_actn.as<int32_t>() + q0, nc, k,
+                     d_gain.as<double>(), d_vals.as<double>() + q0, st));
+  }
+  std::vector<double> vals((size_t)std::max<int64_t>(per_rank, 1) * c->world, 0.0);
+  if (hi > lo)
+    HIPCHK(hipMemcpyAsync(vals.data() + (size_t)c->rank * per_rank, d_vals.as<double>() + lo, (hi - lo) * 8,
+                          hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (c->world > 1) TRYC(allgather_host(c, reinterpret_cast<float*>(vals.data()), per_rank * 2));
+  double sum = 0.0;  // mean over users in ascending id order (RankingMetrics: RDD mean)
+  for (int64_t i = 0; i < nr; ++i) sum += vals[i];
+  *ndcg_out = sum / (double)nr;
+  if (nr <= cap) {
+    if (users_out)
+      for (int64_t i = 0; i < nr; ++i) users_out[i] = S.ids[rows[i]];
+    if (per_user_out) std::memcpy(per_user_out, vals.data(), nr * 8);
   }
   return ALS_OK;
 }

@@ -24,6 +24,7 @@
 #include <utility>
 #include "kernels.h"
 #include "device_common.h"
+#include "wave_chol.h"
 
 namespace albedo {
 
@@ -260,11 +261,13 @@ hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64
 //   K v = C⁻¹ w (register Cholesky, lane i = row i), x' = D⁻¹ Z_jᵀ v.
 // Entries with c = 0 (implicit zero ratings) contribute nothing to A or b and are masked out.
 // =============================================================================================
+// LDS floats per wave: D = 16 keeps K and L as packed lower triangles (+ 64: sink); D = 32 / 64 factor
+// in the MFMA accumulators (wave_chol.h) and need its scratch (512 floats + NB L⁻¹ tiles)
+__host__ __device__ constexpr int light_wave_lds(int D) { return D == 16 ? D * (D + 1) / 2 + 64 : 512 + (D / 16) * 256; }
+
 template <int KP, int D>
-__global__ __launch_bounds__(256, (D == 16 && KP <= 128) ? 6 : (D == 64 && KP == 128) ? 4 : 1) void solve_light_kernel(SolveArgs a) {
-  // K and L live in LDS as packed lower triangles (element (r, c), c <= r, at r(r+1)/2 + c): half the
-  // LDS of a full D x D image, so four D = 64 workgroups fit a CU instead of two
-  constexpr int NB = D / 16, NT = NB * (NB + 1) / 2, TRI = D * (D + 1) / 2 + 64, NHC = KP / 64;  // + 64: sink
+__global__ __launch_bounds__(256, (D == 16 && KP <= 128) ? 6 : (KP <= 128) ? 4 : 2) void solve_light_kernel(SolveArgs a) {
+  constexpr int NB = D / 16, NT = NB * (NB + 1) / 2, TRI = light_wave_lds(D), NHC = KP / 64;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
   float* Ks = smem + wave * TRI;
@@ -390,31 +393,32 @@ __global__ __launch_bounds__(256, (D == 16 && KP <= 128) ? 6 : (D == 64 && KP ==
     }
   }
   if (__any(bad) && lane == 0) atomicOr(a.err, 1);
-  // S -> LDS (only the lower triangle is read by the Cholesky below)
-  static_for<0, NT>([&](auto t) {
-    constexpr TilePair p = upper_tile(decltype(t)::value, NB);
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int row = 16 * p.a + 4 * g + rr, cl = 16 * p.b + i16;  // p.a <= p.b: cl >= row off the diagonal
-      Ks[(p.a < p.b || cl >= row) ? cl * (cl + 1) / 2 + row : TRI - 64 + lane] = acc[t][rr];  // else: sink
-    }
-  });
-  WAVE_LDS_SYNC();
-  const int me = lane < D ? lane : 0;
   const float cinv = valid ? frcp(ce) : 0.f;
-  float kr[D];
+  float y;  // lane e < d: v_e on return
+  if constexpr (D == 16) {  // register Cholesky, lane i = row i, DPP broadcasts
+    // S -> LDS (only the lower triangle is read by the Cholesky below)
+    static_for<0, NT>([&](auto t) {
+      constexpr TilePair p = upper_tile(decltype(t)::value, NB);
 #pragma unroll
-  for (int m = 0; m < D; ++m) {
-    const float v = Ks[me * (me + 1) / 2 + m];  // in bounds for m > me too (unused entries)
-    kr[m] = (m == me) ? (valid ? v + cinv : 1.0f) : (valid ? v : 0.0f);
-  }
-  // Cholesky K = L Lᵀ, lane i holds row i (entries m <= i are L[i][m] when done); then the forward
-  // substitution L y = C⁻¹ w.  D = 16: broadcasts of lane c by DPP row_newbcast (rows 0..15 sit in
-  // lanes 0..15; the other 16-lane rows broadcast their own unused copies); D > 16: readlane.
-  bool notpd = false;
-  float dg = 1.f;  // 1 / L[me][me]
-  float y = valid ? we * cinv : 0.f;
-  if constexpr (D == 16) {
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = 16 * p.a + 4 * g + rr, cl = 16 * p.b + i16;  // p.a <= p.b: cl >= row off the diagonal
+        Ks[(p.a < p.b || cl >= row) ? cl * (cl + 1) / 2 + row : TRI - 64 + lane] = acc[t][rr];  // else: sink
+      }
+    });
+    WAVE_LDS_SYNC();
+    const int me = lane < D ? lane : 0;
+    float kr[D];
+#pragma unroll
+    for (int m = 0; m < D; ++m) {
+      const float v = Ks[me * (me + 1) / 2 + m];  // in bounds for m > me too (unused entries)
+      kr[m] = (m == me) ? (valid ? v + cinv : 1.0f) : (valid ? v : 0.0f);
+    }
+    // Cholesky K = L Lᵀ, lane i holds row i (entries m <= i are L[i][m] when done); then the forward
+    // substitution L y = C⁻¹ w; broadcasts of lane c by DPP row_newbcast (rows 0..15 sit in lanes
+    // 0..15; the other 16-lane rows broadcast their own unused copies)
+    bool notpd = false;
+    float dg = 1.f;  // 1 / L[me][me]
+    y = valid ? we * cinv : 0.f;
     // rows c >= d are identity rows (and y_c = 0): their steps change nothing and are skipped
     static_for<0, D>([&](auto cc) {
       constexpr int c = decltype(cc)::value;
@@ -435,36 +439,18 @@ __global__ __launch_bounds__(256, (D == 16 && KP <= 128) ? 6 : (D == 64 && KP ==
       const float yc = bc16<c>(y * dg);
       y = (me > c) ? fmaf(-kr[c], yc, y) : ((me == c) ? yc : y);
     });
-  } else {
+    if (notpd && lane == 0) atomicOr(a.err, 2);
+    // transpose L through LDS: lane i gets column i (lt[m] = L[m][i])
+    WAVE_LDS_SYNC();
+    if (lane < D) {
 #pragma unroll
-    for (int c = 0; c < D; ++c) {
-      const float piv = rdlane(kr[c], c);
-      if (!(piv > 0.f)) notpd = true;
-      const float inv = frsq(piv), s = piv * inv;
-      kr[c] = (me == c) ? s : kr[c] * inv;
-      dg = (me == c) ? inv : dg;
-#pragma unroll
-      for (int m = c + 1; m < D; ++m) kr[m] = fmaf(-kr[c], rdlane(kr[c], m), kr[m]);
+      for (int m = 0; m < D; ++m) Ks[m <= lane ? lane * (lane + 1) / 2 + m : TRI - 64 + lane] = kr[m];
     }
+    WAVE_LDS_SYNC();
+    float lt[D];
 #pragma unroll
-    for (int c = 0; c < D; ++c) {
-      const float yc = rdlane(y * dg, c);
-      y = (me > c) ? fmaf(-kr[c], yc, y) : ((me == c) ? yc : y);
-    }
-  }
-  if (notpd && lane == 0) atomicOr(a.err, 2);
-  // transpose L through LDS: lane i gets column i (lt[m] = L[m][i])
-  WAVE_LDS_SYNC();
-  if (lane < D) {
-#pragma unroll
-    for (int m = 0; m < D; ++m) Ks[m <= lane ? lane * (lane + 1) / 2 + m : TRI - 64 + lane] = kr[m];
-  }
-  WAVE_LDS_SYNC();
-  float lt[D];
-#pragma unroll
-  for (int m = 0; m < D; ++m) lt[m] = Ks[m * (m + 1) / 2 + me];  // L[m][me] (m >= me used)
-  // backward: Lᵀ v = y
-  if constexpr (D == 16) {
+    for (int m = 0; m < D; ++m) lt[m] = Ks[m * (m + 1) / 2 + me];  // L[m][me] (m >= me used)
+    // backward: Lᵀ v = y
     static_for<0, D>([&](auto cc) {
       constexpr int c = D - 1 - decltype(cc)::value;
       if (c >= d) return;
@@ -472,11 +458,24 @@ __global__ __launch_bounds__(256, (D == 16 && KP <= 128) ? 6 : (D == 64 && KP ==
       y = (me < c) ? fmaf(-lt[c], vc, y) : ((me == c) ? vc : y);
     });
   } else {
+    // K = S + C⁻¹ (identity rows for masked entries), factored in the accumulators (wave_chol.h):
+    // the diagonal of tile (A, A) sits in lane i + 16q, slot r with 4q + r == i
+    const float dadd = valid ? cinv : 1.0f, rhs = valid ? we * cinv : 0.f;
+    float bacc[NB];
+    static_for<0, NB>([&](auto AA) {
+      constexpr int A = decltype(AA)::value, t = tix(A, A, NB);
+      const float dA = __shfl(dadd, 16 * A + i16);
 #pragma unroll
-    for (int c = D - 1; c >= 0; --c) {
-      const float vc = rdlane(y * dg, c);
-      y = (me < c) ? fmaf(-lt[c], vc, y) : ((me == c) ? vc : y);
-    }
+      for (int r = 0; r < 4; ++r)
+        if (4 * g + r == i16) acc[t][r] += dA;
+      bacc[A] = __shfl(rhs, 16 * A + i16);
+    });
+    float xs[NB];
+    const bool notpd = wave_chol_solve<NB>(acc, bacc, Ks, xs);
+    if (notpd && lane == 0) atomicOr(a.err, 2);
+    y = 0.f;  // lane 16A + i holds v[16A + i] = xs[A] (its own slot A = g)
+#pragma unroll
+    for (int A = 0; A < NB; ++A) y = g == A ? xs[A] : y;
   }
   // x' = D⁻¹ Zᵀ v
   if constexpr (KEEPZ) {
@@ -537,7 +536,7 @@ hipError_t launch_solve_light(int KP, int D, const SolveArgs& a0, hipStream_t s)
   }
   const SolveArgs& a = a0;
   const int blocks = (int)((a.n_rows + 3) / 4);
-  const size_t lds = ((size_t)4 * (D * (D + 1) / 2 + 64) + (size_t)4 * KP) * sizeof(float);  // K per wave + D^-1/2
+  const size_t lds = ((size_t)4 * light_wave_lds(D) + (size_t)4 * KP) * sizeof(float);  // per-wave K / scratch + D^-1/2
 #define LIGHT(kp, dd) \
   if (KP == kp && D == dd) { solve_light_kernel<kp, dd><<<blocks, 256, lds, s>>>(a); return hipGetLastError(); }
   LIGHT(64, 16) LIGHT(64, 32) LIGHT(64, 64) LIGHT(128, 16) LIGHT(128, 32) LIGHT(128, 64)

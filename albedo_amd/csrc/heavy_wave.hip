@@ -26,6 +26,7 @@
 #include <cstdint>
 #include "device_common.h"
 #include "kernels.h"
+#include "wave_chol.h"
 
 namespace albedo {
 namespace {
@@ -48,9 +49,6 @@ struct WaveRow {
   static_assert(RPI * RB == 1024 && 8 % RPI == 0, "DMA pieces never cross an 8-rating group");
   static_assert(LDS_WAVE >= 2048 + NQ * 1024, "the stage doubles as the factor's scratch + L⁻¹ store");
 };
-
-// upper tile (a <= b) index, row-major over the upper triangle
-__host__ __device__ constexpr int tix(int a, int b, int nq) { return a * nq - a * (a - 1) / 2 + (b - a); }
 
 // LDS byte offset of (rating r of the stage, column c).  Lane i + 16q reads ratings 8q..8q+7 of
 // column 16A + i: the 64-B shift per 8-rating group puts the four q groups on different banks.
@@ -220,124 +218,9 @@ __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
   if (q == 0) for (int A = 0; A < NQ; ++A) a.X[(int64_t)j * KP + 16 * A + i16] = bacc[A] + acc[tix(A, A, NQ)][0];
   return;
 #endif
-  // ---- blocked Cholesky A' = UᵀU on the tiles; RHS forward substitution alongside ----------------
-  float* scr = reinterpret_cast<float*>(st);  // [0,256): diagonal tile, [256,512): L⁻¹ staging
-  // L⁻¹ of every panel in the A-operand layout (lane i + 16q: L⁻¹[i][4q .. 4q+3]), kept in the dead
-  // stage for the back substitution: [NQ][64 lanes] f32x4 after the two scratch tiles
-  f32x4* s_linv = reinterpret_cast<f32x4*>(scr + 512);
-  bool notpd = false;
-  static_for<0, NQ>([&](auto JB) {
-    constexpr int jb = decltype(JB)::value, td = tix(jb, jb, NQ);
-    // diagonal tile to the row layout of chol16 (lane i: row i, replicated over the 4 lane groups)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) scr[(4 * q + r) * 16 + i16] = acc[td][r];
-    WAVE_LDS_SYNC();
-    float rr[16];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const f32x4 v = ld4(scr + 16 * i16 + 4 * u);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) rr[4 * u + e] = v[e];
-    }
-    float dg = 1.f;
-    notpd |= chol16(rr, dg, i16);
-    // chol16 ends in inline asm: two wait states before any DPP read of its results
-    asm volatile("s_nop 1"
-                 : "+v"(rr[0]), "+v"(rr[1]), "+v"(rr[2]), "+v"(rr[3]), "+v"(rr[4]), "+v"(rr[5]), "+v"(rr[6]),
-                   "+v"(rr[7]), "+v"(rr[8]), "+v"(rr[9]), "+v"(rr[10]), "+v"(rr[11]), "+v"(rr[12]),
-                   "+v"(rr[13]), "+v"(rr[14]), "+v"(rr[15]), "+v"(dg));
-    // column i16 of L⁻¹: L x = e_i16 by forward substitution, L[r][m] broadcast from lane r
-    float x[16];
-    static_for<0, 16>([&](auto RR) {
-      constexpr int r = decltype(RR)::value;
-      float tv = (i16 == r) ? 1.f : 0.f;
-      // one v_fmac_f32_dpp per term (asm keeps the broadcasts from being hoisted into registers)
-      static_for<0, r>([&](auto MM) {
-        constexpr int m = decltype(MM)::value;
-        fnmac_bc16<r, false>(tv, rr[m], x[m]);
-      });
-      x[r] = tv * bc16_after_asm<r>(dg);
-    });
-    if (q == 0) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) scr[256 + 16 * r + i16] = x[r];
-    }
-    WAVE_LDS_SYNC();
-    const f32x4 lv = ld4(scr + 256 + 16 * i16 + 4 * q);
-    s_linv[jb * 64 + lane] = lv;
-    // panel row: U(jb, I) = L⁻¹ T(jb, I)  (A = L⁻¹ rows, B = the tile's C/D registers)
-    static_for<jb + 1, NQ>([&](auto II) {
-      constexpr int I = decltype(II)::value, t = tix(jb, I, NQ);
-      f32x4 u = zero4();
-#pragma unroll
-      for (int s = 0; s < 4; ++s) u = mfma4(lv[s], acc[t][s], u);
-      acc[t] = u;
-    });
-    // RHS: y_jb = L⁻¹ b_jb, then b_M -= U(jb, M)ᵀ y_jb for the blocks below
-    float yp = 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) yp = fmaf(lv[s], __shfl(bacc[jb], 4 * q + s), yp);
-    yp += __shfl_xor(yp, 16);
-    yp += __shfl_xor(yp, 32);
-    bacc[jb] = yp;
-    float y4[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) y4[r] = __shfl(yp, 4 * q + r);
-    static_for<jb + 1, NQ>([&](auto MM) {
-      constexpr int M = decltype(MM)::value, t = tix(jb, M, NQ);
-      float pv = 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) pv = fmaf(acc[t][r], y4[r], pv);
-      pv += __shfl_xor(pv, 16);
-      pv += __shfl_xor(pv, 32);
-      bacc[M] -= pv;
-    });
-    // trailing tiles: T(M, I) -= U(jb, M)ᵀ U(jb, I), the next diagonal tile first
-    static_for<jb + 1, NQ>([&](auto MM) {
-      constexpr int M = decltype(MM)::value, tm = tix(jb, M, NQ);
-      static_for<M, NQ>([&](auto II) {
-        constexpr int I = decltype(II)::value, t = tix(M, I, NQ), ti = tix(jb, I, NQ);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc[t] = mfma4(-acc[tm][s], acc[ti][s], acc[t]);
-      });
-    });
-    WAVE_LDS_SYNC();  // scratch reads done before the next panel rewrites it
-  });
-
-  // ---- back substitution: x_jb = L_jb⁻ᵀ (y_jb - Σ_{M > jb} U(jb, M) x_M) ------------------------
+  // ---- blocked Cholesky A' = UᵀU on the tiles, RHS alongside (wave_chol.h) -----------------------
   float xs[NQ];
-  static_for<0, NQ>([&](auto KK) {
-    constexpr int jb = NQ - 1 - decltype(KK)::value;
-    float pr[4] = {0.f, 0.f, 0.f, 0.f};  // lane c + 16g: Σ_M U(jb, M)[4g + r][c] x_M[c]
-    static_for<jb + 1, NQ>([&](auto MM) {
-      constexpr int M = decltype(MM)::value, t = tix(jb, M, NQ);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) pr[r] = fmaf(acc[t][r], xs[M], pr[r]);
-    });
-    float tq[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) tq[r] = sum16_last(pr[r]);  // row 4g + r in lane 15 + 16g
-    // lane i + 16q gets t_i = y_i - (row i's sum): row i lives in lane 15 + 16(i >> 2), slot i & 3
-    float ti = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float v = __shfl(tq[r], 15 + 16 * (i16 >> 2));
-      ti = (i16 & 3) == r ? v : ti;
-    }
-    ti = bacc[jb] - ti;
-    // x = L⁻ᵀ t: lane k + 16q holds L⁻¹[k][4q + s]; x[4q + s] = Σ_k L⁻¹[k][4q + s] t_k
-    const f32x4 lv = s_linv[jb * 64 + lane];
-    float xq[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) xq[s] = sum16_last(lv[s] * ti);  // x[4g + s] in lane 15 + 16g
-    float xi = 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const float v = __shfl(xq[s], 15 + 16 * (i16 >> 2));
-      xi = (i16 & 3) == s ? v : xi;
-    }
-    xs[jb] = xi;
-  });
+  const bool notpd = wave_chol_solve<NQ>(acc, bacc, reinterpret_cast<float*>(st), xs);
   bool nonfinite = false;
 #pragma unroll
   for (int A = 0; A < NQ; ++A) {

@@ -137,6 +137,21 @@ hipError_t topk_order(int KP, const TopkArgs& a, void* temp, size_t temp_bytes, 
 int topk_rows_per_workgroup(int KP, int64_t n_src, int n_cu);
 // exact full scan for the given src-row indices (rows == null: rows 0 .. n_rows-1), any k <= TOPK_MAX
 hipError_t launch_topk_exact(int KP, const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s);
+// ---- evaluation (eval.hip): RankingEvaluator.scala:83-139 on the device ----------------------------
+size_t eval_sort_temp_bytes(int64_t n);
+// user ids -> rows of the ascending `ids`, grouped: runs[r] (row) with counts[r] entries at
+// idx_sorted[offsets[r] ..]; *n_runs on the device (host copy synchronised inside); the unknown-id run
+// (row 0xFFFFFFFF) is the last one when present
+hipError_t eval_group_users(const int32_t* user, int64_t n, const int32_t* ids, int64_t n_ids, void* temp,
+                            size_t temp_bytes, uint32_t* row, uint32_t* row_sorted, uint32_t* idx, uint32_t* idx_sorted,
+                            uint32_t* runs, int32_t* counts, int64_t* offsets, int64_t* n_runs, hipStream_t s);
+// per run: the first min(k, count) items by (key desc, item asc) -> act [n_runs][k] (-1 padded), act_n
+hipError_t eval_actual_lists(const uint32_t* idx_sorted, const int64_t* offsets, const int32_t* counts, int64_t n_runs,
+                             const int64_t* key, const int32_t* item, int k, int32_t* act, int32_t* act_n,
+                             hipStream_t s);
+// ndcgAt(k) per user of pred [n][k] (raw ids, -1 tail) against act; gain[i] = 1 / ln(i + 2)
+hipError_t eval_ndcg(const int32_t* pred, const int32_t* act, const int32_t* act_n, int64_t n_users, int k,
+                     const double* gain, double* out, hipStream_t s);
 // *out = bits of max_r ||T[r][0..kreal)||_2 computed in fp64
 hipError_t launch_rownorm_max(const float* T, int64_t n, int KP, int kreal, unsigned long long* out, hipStream_t s);
 

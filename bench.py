@@ -202,7 +202,8 @@ def main():
         st1 = np.zeros(4, np.int64)
         L.check(lib.als_topk_stats(h, L.ptr(st1, C.c_int64)))
         dst = st1 - st0
-        topk_info = {"users": int(sub.size), "all_users": bool(every), "seconds": topk_s, "exact_rescan_rows": int(dst[1]),
+        topk_info = {"users": int(sub.size), "all_users": bool(every), "seconds": topk_s,
+                     "sweeps_before_topk": args.warmup + args.steps, "exact_rescan_rows": int(dst[1]),
                      "dst_chunks_scanned_frac": float(dst[2]) / max(1, int(dst[3])),
                      "note": "wall time of als_recommend(k=30) on the user subset: dst norm sort + fp16 pack, "
                              "MFMA scan with norm-order early exit, exact F2J rescoring, D2H of the lists"}

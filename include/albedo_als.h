@@ -138,6 +138,15 @@ int als_model_create(int32_t rank, int64_t n_users, const int32_t* user_ids, con
  * k > 512: ALS_E_UNSUPPORTED. */
 int als_recommend(als_ctx* ctx, int side, int32_t k, const int32_t* subset, int64_t n_subset,
                   int32_t* src_ids_out, int32_t* dst_ids_out, float* scores_out);
+/* RankingEvaluator (RankingEvaluator.scala:83-139) on the device, the albedo protocol of
+ * ALSRecommenderBuilder.scala:92-104: actual lists = intoUserActualItems(user, item, key desc, k) of
+ * the given (user, item, key) rows (key = starred_at; rank() <= k, collect_list, slice(0, k) = the
+ * first k by (key desc, item asc)), restricted to the model's users (inner join); predicted lists =
+ * the users' top-k recommendations (als_recommend, kept on the device); mllib RankingMetrics.ndcgAt(k)
+ * per user and the mean over users (*ndcg_out; NaN when no user is left).  users_out (ascending ids)
+ * and per_user_out are filled when non-null and *n_users_out <= cap.  1 <= k <= 64. */
+int als_evaluate_ndcg(als_ctx* ctx, int32_t k, int64_t n, const int32_t* user, const int32_t* item, const int64_t* key,
+                      double* ndcg_out, int64_t* n_users_out, int32_t* users_out, double* per_user_out, int64_t cap);
 /* ALSModel.transform: F2J sdot per (user, item) pair; NaN when either id is unknown. */
 int als_predict(als_ctx* ctx, int64_t n, const int32_t* user, const int32_t* item, float* out);
 

@@ -453,6 +453,35 @@ def test_topk_subset_unknown_ids_and_small_catalogue(gpu_lib):
         gpu_lib.als_destroy(h)
 
 
+@pytest.mark.parametrize("k", [30, 10])
+def test_device_ndcg_matches_host_evaluator(gpu_lib, k):
+    """RankingEvaluator on the device (als_evaluate_ndcg): actual lists = rank() over starred_at desc
+    (engineered timestamp ties, users with fewer and more than k stars), predicted = the top-k lists,
+    ndcgAt per user bit-identical to the host evaluator (RankingEvaluator.scala:83-139), the mean
+    within 1e-12; users unknown to the model are dropped by the join."""
+    from albedo_amd import ALS
+    from albedo_amd import evaluation as E
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(2500, 600, 40000, seed=19), with_timestamps=True)
+    model = ALS(rank=24, maxIter=3, regParam=0.5, alpha=40.0, implicitPrefs=True).fit(d)
+    rng = np.random.default_rng(k)
+    ts = d["ts"] // 1_000_000  # coarse: many equal timestamps within a user (rank() ties)
+    users = np.r_[d["user"], np.full(5, 123456789, np.int32)]  # an id the model does not know
+    items = np.r_[d["item"], d["item"][:5]]
+    keys = np.r_[ts, ts[:5]]
+    perm = rng.permutation(users.size)  # any input order
+    mean, uids, vals = model.evaluate_ndcg(users[perm], items[perm], keys[perm], k=k, per_user=True)
+    actual = E.into_user_items(users, items, keys, k)
+    src, ids, _ = model.recommend_np(k, subset=uids)
+    assert np.array_equal(src, uids)
+    pred = {int(u): [int(x) for x in ids[r] if x >= 0] for r, u in enumerate(src)}
+    assert 123456789 not in set(uids.tolist()) and uids.size == np.unique(d["user"]).size
+    ref = [E.ndcg_at([(pred[int(u)][:k], actual[int(u)][:k])], k) for u in uids]
+    assert np.array_equal(vals, np.asarray(ref))
+    host = E.RankingEvaluator(actual, "NDCG@k", k).evaluate(pred)
+    assert abs(mean - host) <= 1e-12 * max(1.0, abs(host))
+
+
 def test_transform_bit_exact_and_cold_start(gpu_lib):
     from albedo_amd import ALS
     from albedo_amd.synthetic import SynthSpec, generate

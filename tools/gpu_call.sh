@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU call of this round: steps given as arguments are run in order, each under its own time
 # limit; the call stops at the first failing step.  usage: tools/gpu_call.sh <step> [<step> ...]
-#   bounds_c2 | bounds_c4 | tests_scale | tests_all | smoke | bench_c4 | bench_c2 | bench_c5
+#   bounds_c2 | bounds_c4 | tests_quick | tests_scale | tests_all | smoke | bench_c4 | bench_c2 | bench_c5
 set -e
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
@@ -11,6 +11,7 @@ for s in "$@"; do
   case $s in
     bounds_c2) timeout -k 10 300 python -u tools/topk_bounds.py --config c2 --sweeps 10 --sample 16384 --out gpurun_out/bounds_c2_s10.json > gpurun_out/bounds_c2.log 2>&1 ;;
     bounds_c4) timeout -k 10 500 python -u tools/topk_bounds.py --config c4 --sweeps 25 --sample 16384 --out gpurun_out/bounds_c4_s25.json > gpurun_out/bounds_c4.log 2>&1 ;;
+    tests_quick) timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "half_sweep or golden or facade or albedo_protocol" > gpurun_out/tests_quick.log 2>&1 ;;
     tests_scale) timeout -k 10 900 $PYT tests/test_gpu_scale.py -s > gpurun_out/tests_scale.log 2>&1 ;;
     tests_all) timeout -k 10 1100 $PYT tests -m gpu > gpurun_out/tests_all.log 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke.log 2>&1 ;;
