@@ -75,6 +75,7 @@ SIGNATURES = [
     ("als_create", C.c_int, [C.POINTER(als_params), C.POINTER(P)]),
     ("als_destroy", None, [P]),
     ("als_set_params", C.c_int, [P, C.POINTER(als_params)]),
+    ("als_fork", C.c_int, [P, C.POINTER(als_params), C.POINTER(P)]),
     ("als_last_error", C.c_char_p, []),
     ("als_abi_version", C.c_int, []),
     ("als_device_count", C.c_int, [C.POINTER(C.c_int)]),

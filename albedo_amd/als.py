@@ -197,9 +197,13 @@ class ALS(_Params):
         model.fit_seconds = fit_s
         return model
 
-    def _fit_many(self, dataset, maps):
+    def _fit_many(self, dataset, maps, max_concurrent=8):
+        """The CV grid (ALSRecommenderCV.scala:67-90): one ingest; the maps of one rank are fitted
+        CONCURRENTLY, each on an als_fork of the ingest context (own factors and streams, shared CSR)
+        driven by its own host thread; every model is bit-identical to its standalone fit."""
         if not maps:
             return []
+        from concurrent.futures import ThreadPoolExecutor
         cols = ("userCol", "itemCol", "ratingCol")
         if any(m[c] != maps[0][c] for m in maps for c in cols):
             raise IllegalArgumentException(_lib.ALS_E_INVALID_ARGUMENT,
@@ -207,38 +211,59 @@ class ALS(_Params):
         user, item, rating = self._ratings(dataset, maps[0])
         lib = load()
         h = self._context(maps[0])
-        models = []
+        models = [None] * len(maps)
         try:
             for pm in maps:  # validate every map before the ingest (no fit runs on a bad grid)
                 check(lib.als_set_params(h, C.byref(self._c_params(pm))))
             check(lib.als_set_ratings(h, user.size, ptr(user, C.c_int32), ptr(item, C.c_int32),
                                       ptr(rating, C.c_float)))
-            for pm in maps:
-                check(lib.als_set_params(h, C.byref(self._c_params(pm))))
-                t0 = time.perf_counter()
-                check(lib.als_fit(h))
-                fit_s = time.perf_counter() - t0
-                # snapshot the factors into a model-only context; the ingest context runs the next map
-                k = int(pm["rank"])
-                f = {}
-                for side in (_lib.ALS_USER, _lib.ALS_ITEM):
-                    n = lib.als_num_rows(h, side)
-                    ids = np.empty(n, dtype=np.int32)
-                    fac = np.empty((n, k), dtype=np.float32)
-                    check(lib.als_get_factors(h, side, ptr(ids, C.c_int32), ptr(fac, C.c_float)))
-                    f[side] = (ids, fac)
-                mh = C.c_void_p()
-                (ui, uf), (ii, itf) = f[_lib.ALS_USER], f[_lib.ALS_ITEM]
-                check(lib.als_model_create(k, ui.size, ptr(ui, C.c_int32), ptr(uf, C.c_float), ii.size,
-                                           ptr(ii, C.c_int32), ptr(itf, C.c_float), int(pm["device"]),
-                                           C.byref(mh)))
-                m = ALSModel(mh, pm, uid=self.uid)
-                m._cache.update(f)
-                m.fit_seconds = fit_s
-                models.append(m)
+            groups = {}
+            for i, pm in enumerate(maps):  # forks share the layout of one (rank, nonnegative)
+                groups.setdefault((int(pm["rank"]), bool(pm["nonnegative"])), []).append(i)
+            for idx in groups.values():
+                check(lib.als_set_params(h, C.byref(self._c_params(maps[idx[0]]))))
+                forks = []
+                try:
+                    for i in idx:
+                        fh = C.c_void_p()
+                        check(lib.als_fork(h, C.byref(self._c_params(maps[i])), C.byref(fh)))
+                        forks.append(fh)
+
+                    def run(fh):
+                        t0 = time.perf_counter()
+                        check(lib.als_fit(fh))
+                        return time.perf_counter() - t0
+
+                    with ThreadPoolExecutor(max_workers=max(1, min(max_concurrent, len(forks)))) as ex:
+                        secs = list(ex.map(run, forks))
+                    for i, fh, fit_s in zip(idx, forks, secs):
+                        models[i] = self._snapshot(fh, maps[i], fit_s)
+                finally:
+                    for fh in forks:
+                        lib.als_destroy(fh)
         finally:
             lib.als_destroy(h)
         return models
+
+    def _snapshot(self, h, pm, fit_s):
+        """A model-only context holding the fitted factors of context h (its ingest can then go)."""
+        lib = load()
+        k = int(pm["rank"])
+        f = {}
+        for side in (_lib.ALS_USER, _lib.ALS_ITEM):
+            n = lib.als_num_rows(h, side)
+            ids = np.empty(n, dtype=np.int32)
+            fac = np.empty((n, k), dtype=np.float32)
+            check(lib.als_get_factors(h, side, ptr(ids, C.c_int32), ptr(fac, C.c_float)))
+            f[side] = (ids, fac)
+        mh = C.c_void_p()
+        (ui, uf), (ii, itf) = f[_lib.ALS_USER], f[_lib.ALS_ITEM]
+        check(lib.als_model_create(k, ui.size, ptr(ui, C.c_int32), ptr(uf, C.c_float), ii.size,
+                                   ptr(ii, C.c_int32), ptr(itf, C.c_float), int(pm["device"]), C.byref(mh)))
+        m = ALSModel(mh, pm, uid=self.uid)
+        m._cache.update(f)
+        m.fit_seconds = fit_s
+        return m
 
 
 @_make_accessors

@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <functional>
+#include <mutex>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -32,6 +33,7 @@ using namespace albedo;
 namespace {
 
 thread_local std::string g_err;
+std::mutex g_fork_mu;  // parent / fork lifetimes (als_fork: forks may be destroyed from any thread)
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -59,14 +61,22 @@ int fail(int code, const std::string& msg) {
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  bool owned = true;  // false: a view of another context's buffer (als_fork), never freed here
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p && owned) (void)hipFree(p);
     p = nullptr;
     bytes = 0;
+    owned = true;
+  }
+  void share(const DevBuf& o) {
+    release();
+    p = o.p;
+    bytes = o.bytes;
+    owned = false;
   }
   hipError_t ensure(size_t b) {
     if (b <= bytes && p) return hipSuccess;
@@ -161,6 +171,10 @@ struct als_ctx {
   int slab_blocks = 0;
   hipEvent_t ev[8] = {};
   hipStream_t st2 = nullptr;     // world > 1: factor-chunk gathers behind the solve
+  // als_fork: a fork views its parent's ingest buffers; the parent is freed after its last fork
+  als_ctx* parent = nullptr;
+  int forks = 0;
+  bool doomed = false;
   hipEvent_t evc[9] = {};        // per solve chunk: done on st; [8]: gathers done on st2
 };
 
@@ -318,9 +332,11 @@ int gather_chunk_count() {
 // selects the 4-wave workgroup kernel (A/B measurements); rank 256 always uses the workgroup kernel.
 bool use_wave_kernel(const als_ctx* c);
 
+int factor_buffers(als_ctx* c);
+
 // Everything that depends on the rank / light-row limit rather than on the ratings: degree buckets
-// (the light limit follows KP), factor and rotated-factor buffers, Gram slabs.  Called after ingest
-// and again by als_set_params, so several fits (a CV grid) share one ingest.
+// (the light limit follows KP), split-K lists, then factor_buffers.  Called after ingest and again by
+// als_set_params, so several fits (a CV grid) share one ingest.
 int rank_layout(als_ctx* c) {
   TRYC(drain(c));
   const int64_t lmax = light_limit(c);
@@ -409,6 +425,12 @@ int rank_layout(als_ctx* c) {
       HIPCHK(hipMemcpy(S.d_slot0.p, slot0.data(), slot0.size() * 4, hipMemcpyHostToDevice));
     }
   }
+  return factor_buffers(c);
+}
+
+// Per-fit device state: split-K records, factor / rotated-factor buffers, Gram slabs and scratch;
+// the factors are dropped (the next fit initialises them).
+int factor_buffers(als_ctx* c) {
   {
     const size_t rec = (size_t)split_rec_floats(c->KP) * 4;
     const int64_t mc = std::max(c->s[0].n_chunks, c->s[1].n_chunks);
@@ -1019,6 +1041,11 @@ int als_create(const als_params* p, als_ctx** out) {
 int als_set_params(als_ctx* c, const als_params* p) {
   if (!c || !p) return fail(ALS_E_INVALID_ARGUMENT, "null argument");
   if (c->model_only) return fail(ALS_E_STATE, "als_set_params on a model-only context");
+  if (c->parent) return fail(ALS_E_STATE, "als_set_params on a fork (fork the parent again instead)");
+  {
+    std::lock_guard<std::mutex> lk(g_fork_mu);
+    if (c->forks > 0) return fail(ALS_E_STATE, "als_set_params while forks view this context's layout");
+  }
   TRYC(validate(p));
   TRYC(set_device(c));
   const int dev = c->dev;
@@ -1029,8 +1056,90 @@ int als_set_params(als_ctx* c, const als_params* p) {
   return ALS_OK;
 }
 
+int als_fork(als_ctx* parent, const als_params* p, als_ctx** out) {
+  if (!parent || !p || !out) return fail(ALS_E_INVALID_ARGUMENT, "null argument");
+  *out = nullptr;
+  if (!parent->has_ratings || parent->model_only) return fail(ALS_E_STATE, "als_fork needs a context holding ratings");
+  if (parent->world > 1) return fail(ALS_E_UNSUPPORTED, "als_fork of a sharded (multi-rank) context");
+  TRYC(validate(p));
+  if (p->rank != parent->p.rank || p->nonnegative != parent->p.nonnegative ||
+      p->light_max_degree != parent->p.light_max_degree)
+    return fail(ALS_E_INVALID_ARGUMENT, "a fork keeps its parent's rank, nonnegative and light_max_degree");
+  als_params q = *p;
+  q.device = parent->dev;
+  als_ctx* c = nullptr;
+  TRYC(ctx_common(&q, &c));
+  // the ingest and the rank layout are the parent's (read-only during a fit): views, not copies
+  c->nnz = parent->nnz;
+  c->split_len = parent->split_len;
+  for (int side = 0; side < 2; ++side) {
+    Side& S = c->s[side];
+    const Side& P = parent->s[side];
+    S.n = P.n;
+    S.ids = P.ids;
+    S.starts = P.starts;
+    S.maxrows = P.maxrows;
+    S.nch = P.nch;
+    S.world = P.world;
+    S.chpad = P.chpad;
+    S.own0 = P.own0;
+    S.own_n = P.own_n;
+    S.own_nnz = P.own_nnz;
+    S.h_deg = P.h_deg;
+    S.vmax = P.vmax;
+    S.d_ptr.share(P.d_ptr);
+    S.d_col.share(P.d_col);
+    S.d_val.share(P.d_val);
+    S.d_rows.share(P.d_rows);
+    S.d_chunk_row.share(P.d_chunk_row);
+    S.d_chunk_idx.share(P.d_chunk_idx);
+    S.d_slot0.share(P.d_slot0);
+    std::memcpy(S.boff, P.boff, sizeof S.boff);
+    std::memcpy(S.bnnz, P.bnnz, sizeof S.bnnz);
+    S.n_split = P.n_split;
+    S.n_chunks = P.n_chunks;
+    S.n_batch = P.n_batch;
+    S.n_batch_nnz = P.n_batch_nnz;
+    std::memcpy(S.bat_off, P.bat_off, sizeof S.bat_off);
+    S.nsolve = P.nsolve;
+    std::memcpy(S.cb, P.cb, sizeof S.cb);
+    std::memcpy(S.split_n, P.split_n, sizeof S.split_n);
+    std::memcpy(S.ck_off, P.ck_off, sizeof S.ck_off);
+    std::memcpy(S.sl_off, P.sl_off, sizeof S.sl_off);
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_fork_mu);
+    ++parent->forks;
+  }
+  c->parent = parent;
+  c->has_ratings = true;
+  if (int rc = set_device(c); rc != ALS_OK || (rc = factor_buffers(c)) != ALS_OK) {
+    const std::string msg = g_err;
+    als_destroy(c);
+    return fail(rc, msg);
+  }
+  *out = c;
+  return ALS_OK;
+}
+
+static void destroy_now(als_ctx* c);
+
 void als_destroy(als_ctx* c) {
   if (!c) return;
+  als_ctx* parent_to_free = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_fork_mu);
+    if (c->forks > 0) {  // forks still view this context's ingest: freed with the last of them
+      c->doomed = true;
+      return;
+    }
+    if (c->parent && --c->parent->forks == 0 && c->parent->doomed) parent_to_free = c->parent;
+  }
+  destroy_now(c);
+  if (parent_to_free) destroy_now(parent_to_free);
+}
+
+static void destroy_now(als_ctx* c) {
   (void)hipSetDevice(c->dev);
   if (c->st) (void)hipStreamSynchronize(c->st);
   if (c->st2) (void)hipStreamSynchronize(c->st2);  // no RCCL gather may be in flight at the destroy

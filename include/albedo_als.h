@@ -74,6 +74,14 @@ void als_destroy(als_ctx* ctx);
  * buffers and degree buckets are rebuilt and the factors are dropped, so the next als_fit starts
  * from the new seed's initialisation.  Validated like als_create; the device is kept. */
 int als_set_params(als_ctx* ctx, const als_params* p);
+/* A context that shares `parent`'s ingest (both CSRs, degree buckets, split-K lists: read-only views)
+ * with factors, streams and scratch of its own, for concurrent fits of a CV grid
+ * (ALSRecommenderCV.scala:67-90: several ParamMaps of one rank fitted at once from separate host
+ * threads).  regParam, alpha, maxIter, implicitPrefs and seed may differ from the parent's; rank,
+ * nonnegative and light_max_degree may not.  Single-process contexts only.  The parent's memory stays
+ * allocated until its last fork is destroyed; als_set_params is refused on a fork and on a parent with
+ * live forks. */
+int als_fork(als_ctx* parent, const als_params* p, als_ctx** out);
 const char* als_last_error(void);
 int als_abi_version(void);
 /* number of visible gfx950 devices (0 when no GPU; never initialises a context) */

@@ -280,6 +280,41 @@ def test_param_grid_fit_shares_ingest(gpu_lib):
     assert np.array_equal(one.user_factors_np()[1], models[0].user_factors_np()[1])
 
 
+def test_cv_grid_concurrent_forks(gpu_lib):
+    """ALSRecommenderCV.scala:67-72's grid shape (rank {50, 70} x regParam {0.1, 0.5} x alpha {0.1, 40}):
+    the four maps of each rank run at once on als_fork contexts from four host threads; every model is
+    bit-identical to its standalone fit.  A fork keeps its parent's rank, and the parent's layout is
+    frozen while forks view it."""
+    import ctypes as C
+    from albedo_amd import ALS
+    from albedo_amd import _lib as L
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(1500, 300, 20000, seed=44))
+    grid = [dict(rank=r, regParam=g, alpha=a) for r in (50, 70) for g in (0.1, 0.5) for a in (0.1, 40.0)]
+    base = ALS(implicitPrefs=True, seed=42, maxIter=2)
+    models = base.fit(d, grid)
+    for pm, m in zip(grid, models):
+        solo = ALS(**{**dict(implicitPrefs=True, seed=42, maxIter=2), **pm}).fit(d)
+        for a, b in ((m.user_factors_np(), solo.user_factors_np()), (m.item_factors_np(), solo.item_factors_np())):
+            assert np.array_equal(a[1], b[1]), pm
+    c = Ctx(gpu_lib, 16)
+    c.ratings(d["user"], d["item"], d["rating"])
+    p = L.als_params()
+    L.check(gpu_lib.als_params_default(C.byref(p)))
+    p.rank, p.implicit_prefs = 24, 1
+    f = C.c_void_p()
+    with pytest.raises(L.IllegalArgumentException, match="rank"):
+        L.check(gpu_lib.als_fork(c.h, C.byref(p), C.byref(f)))
+    p.rank = 16
+    L.check(gpu_lib.als_fork(c.h, C.byref(p), C.byref(f)))
+    with pytest.raises(L.IllegalStateException):
+        L.check(gpu_lib.als_set_params(c.h, C.byref(p)))
+    gpu_lib.als_destroy(c.h)  # the parent outlives it: freed with the fork below
+    c.h = None
+    L.check(gpu_lib.als_fit(f))
+    gpu_lib.als_destroy(f)
+
+
 def test_facade_fit_matches_oracle_and_ndcg(gpu_lib):
     from albedo_amd import ALS
     from albedo_amd import evaluation as E
