@@ -110,6 +110,7 @@ struct Side {
   int64_t boff[NBUCKET + 1] = {0};
   int64_t bnnz[NBUCKET] = {0};
   float vmax = 0.f;              // max |rating| over own dst rows (heavy-build fp16 scaling)
+  float vmin = 0.f;              // min |rating| over own dst rows: vmin == vmax -> one confidence c
   DevBuf d_X;                    // [own_n][KP] factors in basis B
   DevBuf d_Z;                    // [prows][KP] rotated factors (src role), gathered layout
   DevBuf d_Xfull;                // world > 1: [prows][KP] every rank's X (basis B), gathered layout
@@ -159,6 +160,7 @@ struct als_ctx {
   bool model_only = false;
   DevBuf slab, d_G, d_P, d_lam, d_err, d_Gt, d_cs, d_csmax;
   DevBuf d_partial, d_reduced;   // split-K partial / reduced A' records (shared by both sides)
+  DevBuf d_Zhl;                  // pre-split src rows of the uniform-confidence heavy build
   DevBuf d_iters;                // NNLS iteration counters (sum, max)
   DevBuf d_gfrag, d_counter;     // lockstep NNLS: G in MFMA operand order, row counter
   int n_cu = 256;
@@ -548,11 +550,13 @@ int ingest_device(als_ctx* c, int64_t n, const int32_t* d_user, const int32_t* d
   TRYC(rank_layout(c));
   for (int side = 0; side < 2; ++side) {
     Side& S = c->s[side];
-    unsigned bits = 0;
+    unsigned bits[2] = {0, 0};
     HIPCHK(launch_absmax(S.d_val.as<float>(), S.own_nnz, c->d_csmax.as<unsigned>(), st));
-    HIPCHK(hipMemcpyAsync(&bits, c->d_csmax.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(launch_absmin(S.d_val.as<float>(), S.own_nnz, c->d_csmax.as<unsigned>() + 1, st));
+    HIPCHK(hipMemcpyAsync(bits, c->d_csmax.p, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    std::memcpy(&S.vmax, &bits, 4);
+    std::memcpy(&S.vmax, &bits[0], 4);
+    std::memcpy(&S.vmin, &bits[1], 4);
   }
   c->has_ratings = true;
   return ALS_OK;
@@ -606,6 +610,34 @@ int column_scales(als_ctx* c, const Side& S, const Side& T) {
 }
 
 int heavy_launches(als_ctx* c, const Side& T, SolveArgs a, int64_t h0, int64_t hn, bool nnls, int q = 0);
+bool use_wave_kernel(const als_ctx* c);
+
+// One confidence c for every rating of dst side T (explicit: c = 1; implicit: all |r| equal): the
+// heavy build's operand split z·√c·colscale -> fp16 hi + lo is then the same for every gather of a
+// src row, so it runs once per src row here (launch_presplit) instead of once per gathered rating
+// inside the wave kernel.  ALBEDO_PRESPLIT=0 keeps the per-rating split (A/B).
+int presplit(als_ctx* c, const Side& S, const Side& T, const void** zhl, float* wsc, float* inv_sw) {
+  static const bool off = [] {
+    const char* e = std::getenv("ALBEDO_PRESPLIT");
+    return e && std::atoi(e) == 0;
+  }();
+  *zhl = nullptr;
+  const bool uniform = !c->p.implicit_prefs || (T.vmin == T.vmax && T.vmax > 0.f);
+  if (off || !uniform || !use_wave_kernel(c) || T.boff[NBUCKET] == T.boff[B_HEAVY]) return ALS_OK;
+  const float cw = c->p.implicit_prefs ? (float)c->p.alpha * T.vmax : 1.0f;
+  if (!(cw > 0.f)) return ALS_OK;
+  const float sw = std::sqrt(cw);
+  HIPCHK(c->d_Zhl.ensure((size_t)(S.prows() + 1) * c->KP * 4));
+  HIPCHK(launch_presplit(c->KP, S.d_Z.as<float>(), S.prows(), c->d_cs.as<float>(), sw, c->d_Zhl.p, c->st));
+  // b' weights w = 1 + c (implicit, r > 0) or r (explicit), scaled by a power of two below 2^13
+  const double wmax = c->p.implicit_prefs ? 1.0 + (double)cw : (double)T.vmax;
+  int e = 0;
+  std::frexp(wmax > 0.0 ? wmax : 1.0, &e);  // wmax < 2^e
+  *wsc = (float)std::ldexp(1.0, std::max(-60, std::min(60, 13 - e)));
+  *inv_sw = 1.0f / sw;
+  *zhl = c->d_Zhl.p;
+  return ALS_OK;
+}
 
 // nonnegative = true: Spark's NNLSSolver in the original basis (no rotation; B stays I)
 int half_sweep_nnls(als_ctx* c, int t) {
@@ -843,9 +875,16 @@ int half_sweep(als_ctx* c, int t) {
   }
   HIPCHK(hipEventRecord(ev[3], st));
   TRYC(column_scales(c, S, T));
+  const void* zhl = nullptr;
+  float wsc = 1.f, inv_sw = 1.f;
+  TRYC(presplit(c, S, T, &zhl, &wsc, &inv_sw));
   HIPCHK(hipEventRecord(ev[4], st));
   HIPCHK(hipMemsetAsync(c->d_err.p, 0, 4, st));
   SolveArgs a{};
+  a.Zhl = zhl;
+  a.zero_row = S.prows();
+  a.wsc = wsc;
+  a.inv_sw = inv_sw;
   a.Z = S.d_Z.as<float>();
   a.ptr = T.d_ptr.as<int64_t>();
   a.col = T.d_col.as<int32_t>();
@@ -1087,6 +1126,7 @@ int als_fork(als_ctx* parent, const als_params* p, als_ctx** out) {
     S.own_nnz = P.own_nnz;
     S.h_deg = P.h_deg;
     S.vmax = P.vmax;
+    S.vmin = P.vmin;
     S.d_ptr.share(P.d_ptr);
     S.d_col.share(P.d_col);
     S.d_val.share(P.d_val);

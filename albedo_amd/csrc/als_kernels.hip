@@ -1511,6 +1511,61 @@ hipError_t launch_colscale(int KP, const float* Z, int64_t n, float cmax, unsign
   return hipGetLastError();
 }
 
+__global__ void absmin_kernel(const float* __restrict__ v, int64_t n, unsigned* __restrict__ out) {
+  float m = INFINITY;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m = fminf(m, fabsf(v[i]));
+  for (int o = 32; o > 0; o >>= 1) m = fminf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) atomicMin(out, __float_as_uint(m));
+}
+
+hipError_t launch_absmin(const float* v, int64_t n, unsigned* out, hipStream_t s) {
+  const unsigned inf = 0x7f800000u;
+  hipError_t e = hipMemcpyAsync(out, &inf, sizeof inf, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);  // `inf` is a stack value
+  if (e != hipSuccess || n <= 0) return e;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  absmin_kernel<<<(int)blocks, 256, 0, s>>>(v, n, out);
+  return hipGetLastError();
+}
+
+// The heavy build's operand split, once per src row: v = z·(sw·cs) (the same two roundings as the
+// per-rating split in solve_wave_kernel), hi = fp16(v), lo = fp16(v - hi); row n is the zero row.
+template <int KP>
+__global__ __launch_bounds__(256) void presplit_kernel(const float* __restrict__ Z, int64_t n,
+                                                       const float* __restrict__ cs, float sw, _Float16* __restrict__ out) {
+  constexpr int CQ = KP / 4;  // float4 chunks per row
+  const int64_t tot = (n + 1) * CQ;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / CQ;
+    const int c4 = (int)(e % CQ) * 4;
+    const f32x4 z = r < n ? ld4(Z + r * KP + c4) : zero4();
+    f16x4 h, l;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      float v = z[m] * (sw * cs[c4 + m]);
+      asm("" : "+v"(v));  // one fp32 rounding; hi and lo both from that value
+      const _Float16 hv = (_Float16)v;
+      h[m] = hv;
+      l[m] = (_Float16)(v - (float)hv);
+    }
+    *reinterpret_cast<f16x4*>(out + r * 2 * KP + c4) = h;
+    *reinterpret_cast<f16x4*>(out + r * 2 * KP + KP + c4) = l;
+  }
+}
+
+hipError_t launch_presplit(int KP, const float* Z, int64_t n, const float* colscale, float sw, void* Zhl, hipStream_t s) {
+  const int64_t tot = (n + 1) * (KP / 4);
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((tot + 255) / 256, 65536));
+  _Float16* o = reinterpret_cast<_Float16*>(Zhl);
+  if (KP == 64) presplit_kernel<64><<<blocks, 256, 0, s>>>(Z, n, colscale, sw, o);
+  else if (KP == 128) presplit_kernel<128><<<blocks, 256, 0, s>>>(Z, n, colscale, sw, o);
+  else if (KP == 256) presplit_kernel<256><<<blocks, 256, 0, s>>>(Z, n, colscale, sw, o);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 hipError_t launch_absmax(const float* v, int64_t n, unsigned* out, hipStream_t s) {
   hipError_t e = hipMemsetAsync(out, 0, sizeof(unsigned), s);
   if (e != hipSuccess || n <= 0) return e;

@@ -55,7 +55,19 @@ struct WaveRow {
 template <int KP>
 __device__ __forceinline__ int soff(int r, int c) { return r * 4 * KP + 64 * (r >> 3) + 4 * c; }
 
-template <int KP, bool IMPLICIT>
+// Pre-split stage layout (PRE): rating row r of the stage holds RB/16 chunks of 16 B (fp16 hi of the
+// row's KP columns, then lo); chunk c sits at chunk position c ^ f(r), f(r) = 2·((r & 3) | ((r & 8) >> 1)).
+// A transposed read (ds_read_b64_tr_b16) of one 16-column block takes, per 32-lane half, 8 rows whose
+// f differ, i.e. 8 distinct 32-B bank windows: conflict-free.
+__device__ __forceinline__ int pre_f(int r) { return 2 * ((r & 3) | ((r & 8) >> 1)); }
+typedef _Float16 f16x4v __attribute__((ext_vector_type(4)));
+typedef __fp16 fp16x4_vs __attribute__((__vector_size__(8)));
+__device__ __forceinline__ f16x4v tr_read(const char* p) {
+  const fp16x4_vs v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) fp16x4_vs*)(p));
+  return __builtin_bit_cast(f16x4v, v);
+}
+
+template <int KP, bool IMPLICIT, bool PRE>
 __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
   using W = WaveRow<KP>;
   constexpr int NQ = W::NQ, NT = W::NT;
@@ -88,6 +100,10 @@ __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
     const int64_t pe = p0 + (e < d ? e : d - 1);
     c_out = a.col[pe];
     r_out = a.val[pe];
+    if constexpr (PRE) {  // past the row end: the zero row (its products vanish in A' and b')
+      c_out = e < d ? c_out : (int)a.zero_row;
+      r_out = e < d ? r_out : 0.f;
+    }
   };
   // gather of one stage: piece u holds ratings RPI·u .. RPI·u + RPI-1, lane l the 16 B at
   // 4·(l % LPR) of rating RPI·u + l / LPR; the rating's src row is wave-uniform (readlane)
@@ -103,8 +119,14 @@ __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
         const int r2 = rdlane_i(cidx, 4 * u + 2), r3 = rdlane_i(cidx, 4 * u + 3);
         row = q == 0 ? r0 : (q == 1 ? r1 : (q == 2 ? r2 : r3));
       }
-      const float* src = a.Z + (int64_t)row * KP + 4 * (lane % W::LPR);
-      __builtin_amdgcn_global_load_lds((glb_vp)src, (lds_vp)(st + soff<KP>(W::RPI * u, 0)), 16, 0, 0);
+      if constexpr (PRE) {
+        const int rr = W::RPI * u + lane / W::LPR;  // row of the stage; chunk position lane % LPR
+        const char* src = reinterpret_cast<const char*>(a.Zhl) + (int64_t)row * W::RB + 16 * ((lane % W::LPR) ^ pre_f(rr));
+        __builtin_amdgcn_global_load_lds((glb_vp)src, (lds_vp)(st + 1024 * u), 16, 0, 0);
+      } else {
+        const float* src = a.Z + (int64_t)row * KP + 4 * (lane % W::LPR);
+        __builtin_amdgcn_global_load_lds((glb_vp)src, (lds_vp)(st + soff<KP>(W::RPI * u, 0)), 16, 0, 0);
+      }
     });
   };
 
@@ -122,41 +144,90 @@ __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
     dma(c_cur);
     if (nst > 1) iload(1, c_nxt, r_nxt);
   }
+  f32x4 bt = zero4();  // PRE: b' of every block in one tile (column 2A: w hi, 2A + 1: w lo)
   for (int s = 0; s < nst; ++s) {
     const bool in = W::SPS * s + (lane & 31) < d;
     npos += __popcll(__ballot(lane < 32 && in && r_cur > 0.f));
     float cw = 0.f, ww = 0.f;
     rating_weights(r_cur, IMPLICIT, a.alpha, cw, ww);
-    const float sw = in ? sqrtf(cw) : 0.f;  // √c (0 past the row end)
-    const float wv = in ? ww : 0.f;
-    float sw8[8];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) sw8[m] = __shfl(sw, 8 * q + m);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this stage's DMA (and stage s+1's indices)
-    // fragment of block A (lane i + 16q: ratings 8q .. 8q+7 of column 16A + i) -> fp16 hi / lo
-    auto conv = [&](auto AA, f16x8& hv, f16x8& lv) {
-      constexpr int A = decltype(AA)::value;
-      float z[8];
-#pragma unroll
-      for (int m = 0; m < 8; ++m) z[m] = *reinterpret_cast<const float*>(st + soff<KP>(8 * q + m, 16 * A + i16));
-      const float csa = s_cs[16 * A + i16];
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        float v = z[m] * (sw8[m] * csa);
-        asm("" : "+v"(v));  // one fp32 rounding; hi and lo both from that value (see heavy_build)
-        const _Float16 h = (_Float16)v;
-        hv[m] = h;
-        lv[m] = (_Float16)(v - (float)h);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // one block's raw values live at a time (register cap)
-    };
     auto tile = [&](auto AA, auto BB, const f16x8& ha, const f16x8& la, const f16x8& hb, const f16x8& lb) {
       constexpr int t = tix(decltype(AA)::value, decltype(BB)::value, NQ);
       acc[t] = mfma_h(ha, hb, acc[t]);
       acc[t] = mfma_h(ha, lb, acc[t]);
       acc[t] = mfma_h(la, hb, acc[t]);
     };
-    {  // every block's fragments in registers (64 VGPRs at KP = 128, beside the tiles' 144)
+    if constexpr (PRE) {
+      // W operand of the b' MFMAs: lane j + 16q holds w of ratings 8q .. 8q+7 (fp16 hi for even j,
+      // lo for odd j), scaled by wsc
+      const float wv = in ? ww * a.wsc : 0.f;
+      f16x8 wop;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        float w = __shfl(wv, 8 * q + m);
+        asm("" : "+v"(w));
+        const _Float16 wh = (_Float16)w;
+        wop[m] = (i16 & 1) ? (_Float16)(w - (float)wh) : wh;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this stage's DMA (and stage s+1's indices)
+      // fragments by transposed reads: lane i + 16q gets column 16A + i of ratings 8q .. 8q+7; lane
+      // 4qq + p of the group addresses row 8q + 4h + qq, columns 4p .. 4p+3 of the block
+      f16x8 fh[NQ], fl[NQ];
+      {
+        const int qq = i16 >> 2, p = i16 & 3;
+        static_for<0, NQ>([&](auto AA) {
+          constexpr int A = decltype(AA)::value;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int r = 8 * q + 4 * h + qq;
+            const char* row = st + r * W::RB + 8 * (p & 1);
+            const int ch = 2 * A + (p >> 1);
+            const f16x4v vh = tr_read(row + 16 * (ch ^ pre_f(r)));
+            const f16x4v vl = tr_read(row + 16 * ((ch + W::RB / 32) ^ pre_f(r)));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              fh[A][4 * h + e] = vh[e];
+              fl[A][4 * h + e] = vl[e];
+            }
+          }
+        });
+      }
+      WAVE_LDS_SYNC();
+      if (s + 1 < nst) next_stage(s);
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<0, NQ>([&](auto AA) {
+        constexpr int A = decltype(AA)::value;
+        static_for<A, NQ>([&](auto BB) {
+          tile(AA, BB, fh[A], fl[A], fh[decltype(BB)::value], fl[decltype(BB)::value]);
+        });
+        const f16x8 wa = ((i16 >> 1) == A) ? wop : f16x8{};
+        bt = mfma_h(fh[A], wa, bt);
+        bt = mfma_h(fl[A], wa, bt);
+      });
+    } else {
+      const float sw = in ? sqrtf(cw) : 0.f;  // √c (0 past the row end)
+      const float wv = in ? ww : 0.f;
+      float sw8[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) sw8[m] = __shfl(sw, 8 * q + m);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this stage's DMA (and stage s+1's indices)
+      // fragment of block A (lane i + 16q: ratings 8q .. 8q+7 of column 16A + i) -> fp16 hi / lo
+      auto conv = [&](auto AA, f16x8& hv, f16x8& lv) {
+        constexpr int A = decltype(AA)::value;
+        float z[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) z[m] = *reinterpret_cast<const float*>(st + soff<KP>(8 * q + m, 16 * A + i16));
+        const float csa = s_cs[16 * A + i16];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          float v = z[m] * (sw8[m] * csa);
+          asm("" : "+v"(v));  // one fp32 rounding; hi and lo both from that value (see heavy_build)
+          const _Float16 h = (_Float16)v;
+          hv[m] = h;
+          lv[m] = (_Float16)(v - (float)h);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one block's raw values live at a time (register cap)
+      };
+      // every block's fragments in registers (64 VGPRs at KP = 128, beside the tiles' 144)
       f16x8 fh[NQ], fl[NQ];
       static_for<0, NQ>([&](auto AA) { conv(AA, fh[decltype(AA)::value], fl[decltype(AA)::value]); });
       // b' += Σ_r w_r z_r: rows read whole (CPL consecutive columns per lane), w_r wave-uniform
@@ -187,13 +258,24 @@ __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
   // ---- b' complete (sum over the four rating groups), tiles unscaled, diagonal Λ + λn ----------
   // b' to the factor's layout (lane i + 16q holds b'[16A + i] for every block A) through LDS
   float* bsc = reinterpret_cast<float*>(st);
-#pragma unroll
-  for (int e = 0; e < CPL; ++e) bsc[CPL * lane + e] = bpart[e];
-  WAVE_LDS_SYNC();
   float bacc[NQ];
+  if constexpr (PRE) {  // bt: lane j + 16q holds column j (block j >> 1, w hi / lo), rows 4q .. 4q+3
 #pragma unroll
-  for (int A = 0; A < NQ; ++A) bacc[A] = bsc[16 * A + i16];
-  WAVE_LDS_SYNC();
+    for (int r = 0; r < 4; ++r) bsc[16 * i16 + 4 * q + r] = bt[r];
+    WAVE_LDS_SYNC();
+    const float ib = a.inv_sw / a.wsc;  // Σ w·(√c·cs·z) / (√c·cs) = b'
+#pragma unroll
+    for (int A = 0; A < NQ; ++A)
+      bacc[A] = (bsc[16 * (2 * A) + i16] + bsc[16 * (2 * A + 1) + i16]) * (s_cs[KP + 16 * A + i16] * ib);
+    WAVE_LDS_SYNC();
+  } else {
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) bsc[CPL * lane + e] = bpart[e];
+    WAVE_LDS_SYNC();
+#pragma unroll
+    for (int A = 0; A < NQ; ++A) bacc[A] = bsc[16 * A + i16];
+    WAVE_LDS_SYNC();
+  }
   const float lamn = a.reg * (float)(IMPLICIT ? npos : d);
   const float* isc = s_cs + KP;
   static_for<0, NQ>([&](auto AA) {
@@ -236,13 +318,20 @@ __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
 template <int KP>
 hipError_t launch_wave_kp(const SolveArgs& a, hipStream_t s) {
   using W = WaveRow<KP>;
-  static const hipError_t attr = allow_lds(solve_wave_kernel<KP, true>, W::LDS);
-  static const hipError_t attr2 = allow_lds(solve_wave_kernel<KP, false>, W::LDS);
-  if (attr != hipSuccess) return attr;
-  if (attr2 != hipSuccess) return attr2;
+  static const hipError_t attr = allow_lds(solve_wave_kernel<KP, true, false>, W::LDS);
+  static const hipError_t attr2 = allow_lds(solve_wave_kernel<KP, false, false>, W::LDS);
+  static const hipError_t attr3 = allow_lds(solve_wave_kernel<KP, true, true>, W::LDS);
+  static const hipError_t attr4 = allow_lds(solve_wave_kernel<KP, false, true>, W::LDS);
+  for (hipError_t e : {attr, attr2, attr3, attr4})
+    if (e != hipSuccess) return e;
   const int blocks = (int)((a.n_rows + W::WAVES - 1) / W::WAVES);
-  if (a.implicit) solve_wave_kernel<KP, true><<<blocks, 64 * W::WAVES, W::LDS, s>>>(a);
-  else solve_wave_kernel<KP, false><<<blocks, 64 * W::WAVES, W::LDS, s>>>(a);
+  if (a.Zhl) {
+    if (a.implicit) solve_wave_kernel<KP, true, true><<<blocks, 64 * W::WAVES, W::LDS, s>>>(a);
+    else solve_wave_kernel<KP, false, true><<<blocks, 64 * W::WAVES, W::LDS, s>>>(a);
+  } else {
+    if (a.implicit) solve_wave_kernel<KP, true, false><<<blocks, 64 * W::WAVES, W::LDS, s>>>(a);
+    else solve_wave_kernel<KP, false, false><<<blocks, 64 * W::WAVES, W::LDS, s>>>(a);
+  }
   return hipGetLastError();
 }
 

@@ -26,6 +26,12 @@ struct SolveArgs {
   const float* colscale;   // [2*KP] heavy-build fp16 column scales 2^e and their inverses
   const float* prebuilt;   // split rows: reduced A' records [n_rows][split_rec_floats] (else null)
   unsigned long long* iters;  // NNLS: [0] += iterations of every row, [1] = max over rows (or null)
+  // uniform confidence (every rating of the side has the same c: binary implicit data, or explicit):
+  // the heavy build gathers pre-split rows instead of Z (launch_presplit), null otherwise
+  const void* Zhl;         // [*][2·KP] fp16: hi of √c·colscale·z, then lo
+  int64_t zero_row;        // an all-zero row of Zhl (the gather target of ratings past a row's end)
+  float wsc;               // power-of-two scale of the rating weights w in the b' MFMA (max|w|·wsc < 2^13)
+  float inv_sw;            // 1 / √c
 };
 
 // Split-K of the heavy tail (rows with more ratings than one chunk): every chunk of chunk_len
@@ -76,8 +82,13 @@ hipError_t launch_nnls_batch(int KP, int slots, const SolveArgs& a, const void* 
 // colscale[c] = 2^e_c with max_rows |Z[.][c]|·√cmax < 2^13, colscale[KP+c] = 2^-e_c (tmp: KP uints)
 hipError_t launch_colscale(int KP, const float* Z, int64_t n, float cmax, unsigned* tmp, float* colscale,
                            hipStream_t s);
+// Zhl[r] = fp16 hi and lo of Z[r][c]·(sw·colscale[c]) (the heavy build's operand split, done once per
+// src row instead of once per gathered rating); row n (the zero row) is cleared
+hipError_t launch_presplit(int KP, const float* Z, int64_t n, const float* colscale, float sw, void* Zhl, hipStream_t s);
 // *out = bits of max |v[i]| (non-negative float, compared as unsigned)
 hipError_t launch_absmax(const float* v, int64_t n, unsigned* out, hipStream_t s);
+// *out = bits of min |v[i]| (0x7f800000 when n = 0)
+hipError_t launch_absmin(const float* v, int64_t n, unsigned* out, hipStream_t s);
 int nnls_gtile_index(int r, int c);  // block(r) >= block(c): NNLS tile layout, diagonal tiles full
 
 // Seeded unit-norm Gaussian rows (global row index row0 + r) for large synthetic runs.
