@@ -765,7 +765,7 @@ int heavy_launches(als_ctx* c, const Side& T, SolveArgs a, int64_t h0, int64_t h
     sp.n_split = ns;
     sp.partial = c->d_partial.as<float>();
     sp.reduced = c->d_reduced.as<float>();
-    HIPCHK(launch_heavy_split(KP, a, sp, c->st));
+    HIPCHK(launch_heavy_split(KP, a, sp, use_wave_kernel(c), c->st));
     SolveArgs b = a;
     b.rows = rows + h0;
     b.n_rows = ns;

@@ -25,6 +25,7 @@
 #include "kernels.h"
 #include "device_common.h"
 #include "wave_chol.h"
+#include "split_rec.h"
 
 namespace albedo {
 
@@ -566,9 +567,6 @@ hipError_t launch_solve_light(int KP, int D, const SolveArgs& a0, hipStream_t s)
 //          b' is carried as an extra row, so the forward substitution comes for free.
 //  back    Lᵀx = y by one wave, no barriers.
 // =============================================================================================
-constexpr int HT_LD = 17, HT_SZ = 16 * HT_LD;
-__device__ __forceinline__ int htile(int I, int J) { return (I * (I + 1) / 2 + J) * HT_SZ; }
-__device__ __forceinline__ int hel(int r, int c) { return htile(r >> 4, c >> 4) + (r & 15) * HT_LD + (c & 15); }
 
 
 template <int KP>
@@ -805,12 +803,6 @@ __device__ __forceinline__ void heavy_build_all(const SolveArgs& a, int64_t p0, 
 }
 
 // ---- split-K records (kernels.h SplitArgs): packed A' tiles | b' | positive-rating count ------
-template <int KP>
-struct SplitRec {
-  static constexpr int TILES = Heavy<KP>::NTL * HT_SZ;
-  static constexpr int OFF_B = TILES, OFF_N = OFF_B + KP;
-  static constexpr int FLOATS = (OFF_N + 1 + 3) & ~3;  // 16-B aligned records
-};
 int split_rec_floats(int KP) {
   return KP == 64 ? SplitRec<64>::FLOATS : KP == 128 ? SplitRec<128>::FLOATS : SplitRec<256>::FLOATS;
 }
@@ -881,22 +873,27 @@ __global__ __launch_bounds__(256) void heavy_reduce_kernel(SplitArgs s) {
 }
 
 template <int KP>
-hipError_t launch_split_kp(const SolveArgs& a, const SplitArgs& s, hipStream_t st) {
+hipError_t launch_split_kp(const SolveArgs& a, const SplitArgs& s, bool wave, hipStream_t st) {
   using R = SplitRec<KP>;
-  const size_t lds = Heavy<KP>::FLOATS * 4;
-  static const hipError_t attr = allow_lds(heavy_partial_kernel<KP>, lds);
-  if (attr != hipSuccess) return attr;
-  heavy_partial_kernel<KP><<<(int)s.n_chunks, Heavy<KP>::NTH, lds, st>>>(a, s);
+  if (wave && KP <= 128) {
+    const hipError_t e = launch_wave_partial(KP, a, s, st);
+    if (e != hipSuccess) return e;
+  } else {
+    const size_t lds = Heavy<KP>::FLOATS * 4;
+    static const hipError_t attr = allow_lds(heavy_partial_kernel<KP>, lds);
+    if (attr != hipSuccess) return attr;
+    heavy_partial_kernel<KP><<<(int)s.n_chunks, Heavy<KP>::NTH, lds, st>>>(a, s);
+  }
   const int gy = (int)(s.n_split < 65535 ? s.n_split : 65535);
   heavy_reduce_kernel<KP><<<dim3((R::OFF_N + 1 + 255) / 256, gy), 256, 0, st>>>(s);
   return hipGetLastError();
 }
 
-hipError_t launch_heavy_split(int KP, const SolveArgs& a, const SplitArgs& s, hipStream_t st) {
+hipError_t launch_heavy_split(int KP, const SolveArgs& a, const SplitArgs& s, bool wave, hipStream_t st) {
   if (s.n_chunks <= 0 || s.n_split <= 0) return hipSuccess;
-  if (KP == 64) return launch_split_kp<64>(a, s, st);
-  if (KP == 128) return launch_split_kp<128>(a, s, st);
-  if (KP == 256) return launch_split_kp<256>(a, s, st);
+  if (KP == 64) return launch_split_kp<64>(a, s, wave, st);
+  if (KP == 128) return launch_split_kp<128>(a, s, wave, st);
+  if (KP == 256) return launch_split_kp<256>(a, s, wave, st);
   return hipErrorInvalidValue;
 }
 

@@ -27,6 +27,7 @@
 #include "device_common.h"
 #include "kernels.h"
 #include "wave_chol.h"
+#include "split_rec.h"
 
 namespace albedo {
 namespace {
@@ -67,25 +68,18 @@ __device__ __forceinline__ f16x4v tr_read(const char* p) {
   return __builtin_bit_cast(f16x4v, v);
 }
 
+// The build of one row's (or split-K chunk's) normal equation by one wave: ratings p0 .. p0+d-1 of
+// the CSR, gathered 32 per stage into this wave's LDS stage st.  On return acc holds the NT upper
+// tiles of Σ c·(cs z)(cs z)ᵀ (still column-scaled), bacc[A] (lane i + 16q) b'[16A + i] unscaled;
+// returns the number of positive ratings.
 template <int KP, bool IMPLICIT, bool PRE>
-__global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
+__device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d, char* st, const float* s_cs,
+                                          f32x4 (&acc)[WaveRow<KP>::NT], float (&bacc)[WaveRow<KP>::NQ]) {
   using W = WaveRow<KP>;
   constexpr int NQ = W::NQ, NT = W::NT;
-  extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63, q = lane >> 4, i16 = lane & 15;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // scalar: LDS-DMA bases in SGPRs
-  float* s_cs = reinterpret_cast<float*>(lds + W::WAVES * W::LDS_WAVE);  // [KP] scales, [KP] inverses
-  for (int e = threadIdx.x; e < 2 * KP; e += 256) s_cs[e] = a.colscale[e];
-  __syncthreads();  // the only workgroup barrier: every wave below is on its own row
-  const int64_t ridx = (int64_t)blockIdx.x * W::WAVES + wave;
-  if (ridx >= a.n_rows) return;
-  char* st = lds + wave * W::LDS_WAVE;
-  const int j = a.rows[ridx];
-  const int64_t p0 = a.ptr[j];
-  const int d = (int)(a.ptr[j + 1] - p0);
   const int nst = (d + W::SPS - 1) / W::SPS;
 
-  f32x4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = zero4();
   constexpr int CPL = KP / 64;  // b' columns per lane during the build: lane l sums CPL·l .. CPL·l+CPL-1
@@ -258,7 +252,6 @@ __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
   // ---- b' complete (sum over the four rating groups), tiles unscaled, diagonal Λ + λn ----------
   // b' to the factor's layout (lane i + 16q holds b'[16A + i] for every block A) through LDS
   float* bsc = reinterpret_cast<float*>(st);
-  float bacc[NQ];
   if constexpr (PRE) {  // bt: lane j + 16q holds column j (block j >> 1, w hi / lo), rows 4q .. 4q+3
 #pragma unroll
     for (int r = 0; r < 4; ++r) bsc[16 * i16 + 4 * q + r] = bt[r];
@@ -276,6 +269,28 @@ __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
     for (int A = 0; A < NQ; ++A) bacc[A] = bsc[16 * A + i16];
     WAVE_LDS_SYNC();
   }
+  return npos;
+}
+
+template <int KP, bool IMPLICIT, bool PRE>
+__global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
+  using W = WaveRow<KP>;
+  constexpr int NQ = W::NQ, NT = W::NT;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int lane = threadIdx.x & 63, q = lane >> 4, i16 = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // scalar: LDS-DMA bases in SGPRs
+  float* s_cs = reinterpret_cast<float*>(lds + W::WAVES * W::LDS_WAVE);  // [KP] scales, [KP] inverses
+  for (int e = threadIdx.x; e < 2 * KP; e += 256) s_cs[e] = a.colscale[e];
+  __syncthreads();  // the only workgroup barrier: every wave below is on its own row
+  const int64_t ridx = (int64_t)blockIdx.x * W::WAVES + wave;
+  if (ridx >= a.n_rows) return;
+  char* st = lds + wave * W::LDS_WAVE;
+  const int j = a.rows[ridx];
+  const int64_t p0 = a.ptr[j];
+  const int d = (int)(a.ptr[j + 1] - p0);
+  f32x4 acc[NT];
+  float bacc[NQ];
+  const int npos = wave_build<KP, IMPLICIT, PRE>(a, p0, d, st, s_cs, acc, bacc);
   const float lamn = a.reg * (float)(IMPLICIT ? npos : d);
   const float* isc = s_cs + KP;
   static_for<0, NQ>([&](auto AA) {
@@ -335,7 +350,83 @@ hipError_t launch_wave_kp(const SolveArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Split-K partial of one chunk per WAVE (kernels.h SplitArgs): the wave build of the chunk's
+// chunk_len ratings, unscaled, into the fp32 record the fp64 chunk-order reduction sums.  Upper tile
+// (A, B) in the C/D layout is stored as lower tile (B, A): lane i + 16q, slot r holds element
+// (16B + i, 16A + 4q + r); diagonal-tile entries above the diagonal and the pad column are zeros.
+template <int KP, bool IMPLICIT, bool PRE>
+__global__ __launch_bounds__(256, 2) void wave_partial_kernel(SolveArgs a, SplitArgs sp) {
+  using W = WaveRow<KP>;
+  using R = SplitRec<KP>;
+  constexpr int NQ = W::NQ, NT = W::NT;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int lane = threadIdx.x & 63, q = lane >> 4, i16 = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* s_cs = reinterpret_cast<float*>(lds + W::WAVES * W::LDS_WAVE);
+  for (int e = threadIdx.x; e < 2 * KP; e += 256) s_cs[e] = a.colscale[e];
+  __syncthreads();
+  const int64_t slot = (int64_t)blockIdx.x * W::WAVES + wave;
+  if (slot >= sp.n_chunks) return;
+  char* st = lds + wave * W::LDS_WAVE;
+  const int j = sp.chunk_row[slot];
+  const int64_t rp0 = a.ptr[j], off = (int64_t)sp.chunk_idx[slot] * sp.chunk_len;
+  const int64_t rest = a.ptr[j + 1] - rp0 - off;
+  const int d = (int)(rest < sp.chunk_len ? rest : sp.chunk_len);
+  f32x4 acc[NT];
+  float bacc[NQ];
+  const int npos = wave_build<KP, IMPLICIT, PRE>(a, rp0 + off, d, st, s_cs, acc, bacc);
+  float* out = sp.partial + slot * R::FLOATS;
+  const float* isc = s_cs + KP;
+  static_for<0, NQ>([&](auto AA) {
+    constexpr int A = decltype(AA)::value;
+    const f32x4 ir = ld4(isc + 16 * A + 4 * q);
+    static_for<A, NQ>([&](auto BB) {
+      constexpr int B = decltype(BB)::value, t = tix(A, B, NQ);
+      const float ic = isc[16 * B + i16];
+      float* tl = out + htile(B, A) + i16 * HT_LD;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool valid = A < B || 4 * q + r <= i16;
+        tl[4 * q + r] = valid ? acc[t][r] * ir[r] * ic : 0.f;
+      }
+      if (q == 0) tl[16] = 0.f;
+    });
+  });
+  if (q == 0) {
+#pragma unroll
+    for (int A = 0; A < NQ; ++A) out[R::OFF_B + 16 * A + i16] = bacc[A];
+  }
+  if (lane == 0) reinterpret_cast<int*>(out)[R::OFF_N] = npos;
+}
+
+template <int KP>
+hipError_t launch_wave_partial_kp(const SolveArgs& a, const SplitArgs& sp, hipStream_t s) {
+  using W = WaveRow<KP>;
+  static const hipError_t e1 = allow_lds(wave_partial_kernel<KP, true, false>, W::LDS);
+  static const hipError_t e2 = allow_lds(wave_partial_kernel<KP, false, false>, W::LDS);
+  static const hipError_t e3 = allow_lds(wave_partial_kernel<KP, true, true>, W::LDS);
+  static const hipError_t e4 = allow_lds(wave_partial_kernel<KP, false, true>, W::LDS);
+  for (hipError_t e : {e1, e2, e3, e4})
+    if (e != hipSuccess) return e;
+  const int blocks = (int)((sp.n_chunks + W::WAVES - 1) / W::WAVES);
+  if (a.Zhl) {
+    if (a.implicit) wave_partial_kernel<KP, true, true><<<blocks, 64 * W::WAVES, W::LDS, s>>>(a, sp);
+    else wave_partial_kernel<KP, false, true><<<blocks, 64 * W::WAVES, W::LDS, s>>>(a, sp);
+  } else {
+    if (a.implicit) wave_partial_kernel<KP, true, false><<<blocks, 64 * W::WAVES, W::LDS, s>>>(a, sp);
+    else wave_partial_kernel<KP, false, false><<<blocks, 64 * W::WAVES, W::LDS, s>>>(a, sp);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
+
+hipError_t launch_wave_partial(int KP, const SolveArgs& a, const SplitArgs& s, hipStream_t st) {
+  if (s.n_chunks <= 0) return hipSuccess;
+  if (KP == 64) return launch_wave_partial_kp<64>(a, s, st);
+  if (KP == 128) return launch_wave_partial_kp<128>(a, s, st);
+  return hipErrorInvalidValue;
+}
 
 hipError_t launch_solve_wave(int KP, const SolveArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;

@@ -49,8 +49,10 @@ struct SplitArgs {
   float* reduced;            // [n_split][split_rec_floats]
 };
 int split_rec_floats(int KP);
-// partial builds of every chunk, then the fp64 reduction into s.reduced
-hipError_t launch_heavy_split(int KP, const SolveArgs& a, const SplitArgs& s, hipStream_t st);
+// partial builds of every chunk (wave: one wave per chunk, heavy_wave.hip, KP <= 128; else one
+// 4/16-wave workgroup per chunk), then the fp64 reduction into s.reduced
+hipError_t launch_heavy_split(int KP, const SolveArgs& a, const SplitArgs& s, bool wave, hipStream_t st);
+hipError_t launch_wave_partial(int KP, const SolveArgs& a, const SplitArgs& s, hipStream_t st);
 
 // G (fp64 [KP][KP], full symmetric) = Σ_rows Xᵀ X over rows [0, n) of X ([n][KP]).
 hipError_t launch_gram(int KP, const float* X, int64_t n, double* slab, int slab_blocks, double* G,
