@@ -1448,6 +1448,19 @@ struct TopkPlan {
   DevBuf d_src, d_ls, d_li, d_lc, d_need, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp, d_thr;
 };
 
+// The scan prunes against the kt-th best candidate so far, not the 64th: certification needs a gap
+// between the k-th exact score and the kt-th approximate one (~1e-3 relative), and k + 16 leaves one
+// while the threshold rises faster than at 64 (fewer dst chunks scanned once the factors converge).
+// The lists still hold 64 and the best 64 are rescored.  ALBEDO_TOPK_KT overrides (k .. 64).
+int topk_threshold_rank(int k) {
+  static const int env = [] {
+    const char* e = std::getenv("ALBEDO_TOPK_KT");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int kt = env > 0 ? env : k + 16;
+  return std::max(k, std::min(TOPK_KC, kt));
+}
+
 int topk_plan(als_ctx* c, int src, int k, TopkPlan& P) {
   P.src = src;
   P.k = k;
@@ -1525,6 +1538,7 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int3
   a.dst_ids = P.d_dstids.as<int32_t>();
   a.kreal = c->p.rank;
   a.k = k;
+  a.kt = topk_threshold_rank(k);
   a.tmax_norm = (float)(P.tmax * (1.0 + 1e-6));
   a.Th = P.d_th.p;
   a.head = P.d_head.as<float>();

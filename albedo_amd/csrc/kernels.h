@@ -112,6 +112,7 @@ struct TopkArgs {
   const int32_t* dst_ids;  // raw ids of dst rows (ascending with the row index)
   int kreal;
   int k;                   // requested top-k
+  int kt;                  // rank of the running threshold in the candidate lists (k <= kt <= TOPK_KC)
   float tmax_norm;         // max_j ||T_j||_2 (for the error bound)
   const void* Th;          // [n_chunks * chunk rows][KP] fp16: T[perm[p]]·tsc, zero rows past n_dst
   const float* head;       // [n_chunks] ||T_{perm[c·chunk]}||, rounded up (0 past n_dst)

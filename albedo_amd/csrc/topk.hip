@@ -320,8 +320,8 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       wave_bitonic<NSC>(s2, i2);
       a.lscore[lb + lane] = s2[0];
       a.lidx[lb + lane] = i2[0];
-      const float t64 = rdlane(s2[0], 63);
-      if (lane == 0) s_thr[wr0 + wl] = t64;
+      const float tkt = rdlane(s2[0], a.kt - 1);  // the running kt-th best becomes the threshold
+      if (lane == 0) s_thr[wr0 + wl] = tkt;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     WAVE_LDS_SYNC();
@@ -430,7 +430,7 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
     i2[h] = e < cnt ? a.lidx[si * CAP + e] : -1;
   }
   wave_bitonic<NS>(s2, i2);
-  const float t = rdlane(s2[0], 63);  // the 64th approximate score (-inf when fewer)
+  const float t = rdlane(s2[0], a.kt - 1);  // the kt-th approximate score (-inf when fewer)
   const int row = i2[0] >= 0 ? a.perm[i2[0]] : -1;
   float ex = -INFINITY;
   if (row >= 0) ex = f2j_dot_v4(s, a.T + (int64_t)row * KP, a.kreal);
@@ -456,7 +456,7 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
     const double e = rel * ns * tm + absu;
     // fewer than 64 listed (a scan that stopped before 64 rows reached a starting threshold): the
     // bound below needs t >= the last threshold, which only a full list guarantees
-    if (cnt < TOPK_KC || !((double)kth > (double)t + e)) {
+    if (cnt < a.kt || !((double)kth > (double)t + e)) {
       if (lane == 0) a.need_exact[so] = 1;
     }
   }
@@ -524,14 +524,14 @@ __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_
   float vs[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    uint32_t lo = 0u, hi = 0xffffffffu;  // count(>= lo) >= 64 always holds (256 keys >= 0)
+    uint32_t lo = 0u, hi = 0xffffffffu;  // count(>= lo) >= kt always holds (256 keys >= 0)
     for (int it = 0; it < 32; ++it) {
       const uint32_t mid = lo + (uint32_t)(((uint64_t)hi - lo + 1) >> 1);
       int cnt = 0;
 #pragma unroll
       for (int J = 0; J < 16; ++J) cnt += u[J][r] >= mid ? 1 : 0;
       for (int o = 1; o < 16; o <<= 1) cnt += __shfl_xor(cnt, o);
-      if (cnt >= 64) lo = mid;
+      if (cnt >= a.kt) lo = mid;
       else hi = mid - 1u;
     }
     vs[r] = __uint_as_float((lo & 0x80000000u) ? (lo & 0x7fffffffu) : ~lo);

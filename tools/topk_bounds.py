@@ -75,8 +75,14 @@ def main():
     ap.add_argument("--sample", type=int, default=16384)
     ap.add_argument("--out", default="gpurun_out/bounds.json")
     ap.add_argument("--fake", action="store_true")
+    ap.add_argument("--npz", default=None, help="analyse saved factors (U, V, udeg) on the CPU")
     args = ap.parse_args()
-    if args.fake:  # CPU dry run of the analysis on random factors
+    if args.npz:
+        z = np.load(args.npz)
+        U, V, deg_u = z["U"], z["V"], z["udeg"]
+        k = U.shape[1]
+        dev = torch.device("cpu")
+    elif args.fake:  # CPU dry run of the analysis on random factors
         rng0 = np.random.default_rng(0)
         k = 64
         U = rng0.standard_normal((20000, k)).astype(np.float32)
