@@ -1424,14 +1424,14 @@ int als_model_create(int32_t rank, int64_t nu, const int32_t* uids, const float*
 }
 
 // top-k experiment switches, read once: ALBEDO_TOPK_DRAIN=1 (wait for every DMA each chunk),
-// ALBEDO_TOPK_ORDER=0 (no scan order / starting thresholds), ALBEDO_TOPK_THR0=0 (order only)
+// ALBEDO_TOPK_THR0=0 (no starting thresholds), ALBEDO_TOPK_PRUNE=0 (no chunk bound: every chunk)
 struct TopkKnobs {
   int drain = 0;
-  bool order = true, thr0 = true;
+  bool thr0 = true, prune = true;
   TopkKnobs() {
     if (const char* e = std::getenv("ALBEDO_TOPK_DRAIN")) drain = std::atoi(e);
-    if (const char* e = std::getenv("ALBEDO_TOPK_ORDER")) order = std::atoi(e) != 0;
     if (const char* e = std::getenv("ALBEDO_TOPK_THR0")) thr0 = std::atoi(e) != 0;
+    if (const char* e = std::getenv("ALBEDO_TOPK_PRUNE")) prune = std::atoi(e) != 0;
   }
 };
 
@@ -1443,10 +1443,35 @@ struct TopkPlan {
   bool exact_only = false;
   double tmax = 0.0, smax = 0.0, ssc = 1.0, tsc = 1.0;
   int CH = 0;
-  int64_t n_chunks = 0;
-  DevBuf d_th, d_head, d_keys, d_perm, d_tmp, d_dstids;
-  DevBuf d_src, d_ls, d_li, d_lc, d_need, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp, d_thr;
+  int64_t n_chunks = 0, n_super = 0;
+  bool prune = false;
+  DevBuf d_th, d_keys, d_perm, d_nperm, d_tp, d_tmp, d_dstids, d_VP, d_cfeat, d_supf, d_probe, d_slab, d_G;
+  DevBuf d_src, d_ls, d_li, d_lc, d_need, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp, d_thr, d_sf, d_mask;
 };
+
+// The leading TOPK_M eigenvectors of the dst side's Gram Σ t tᵀ (original basis), fp64 [TOPK_M][KP]:
+// the directions the top-k chunk bound keeps exactly (topk.hip).
+int topk_dst_basis(als_ctx* c, const Side& T, TopkPlan& P, std::vector<double>& VP) {
+  const int KP = c->KP, k = c->p.rank;
+  const int nblk = gram_slab_blocks(KP, T.n);
+  HIPCHK(P.d_slab.ensure(gram_slab_doubles(KP, nblk) * 8));
+  HIPCHK(P.d_G.ensure((size_t)KP * KP * 8));
+  HIPCHK(launch_gram(KP, T.d_orig.as<float>(), T.n, P.d_slab.as<double>(), nblk, P.d_G.as<double>(), c->st));
+  std::vector<double> Gf((size_t)KP * KP), Gk((size_t)k * k), w(k), V((size_t)k * k);
+  HIPCHK(hipMemcpyAsync(Gf.data(), P.d_G.p, Gf.size() * 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  for (int i = 0; i < k; ++i)
+    for (int j = 0; j < k; ++j) Gk[(size_t)i * k + j] = Gf[(size_t)i * KP + j];
+  if (!sym_eig(k, Gk.data(), w.data(), V.data()))
+    return fail(ALS_E_NOT_POSITIVE_DEFINITE, "eigendecomposition of the dst Gram matrix did not converge");
+  std::vector<int> idx(k);
+  std::iota(idx.begin(), idx.end(), 0);
+  std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return w[a] > w[b]; });
+  VP.assign((size_t)TOPK_M * KP, 0.0);
+  for (int d = 0; d < TOPK_M && d < k; ++d)
+    for (int i = 0; i < k; ++i) VP[(size_t)d * KP + i] = V[(size_t)i * k + idx[d]];
+  return ALS_OK;
+}
 
 // The scan prunes against the kt-th best candidate so far, not the 64th: certification needs a gap
 // between the k-th exact score and the kt-th approximate one (~1e-3 relative), and k + 16 leaves one
@@ -1493,17 +1518,33 @@ int topk_plan(als_ctx* c, int src, int k, TopkPlan& P) {
   P.tsc = pow2_scale(P.tmax);
   // dst side in descending-norm order, fp16 rows + chunk head norms (also for k > 64: the exact scan
   // visits the dst rows in this norm order and stops early)
+  static const TopkKnobs tk;
   P.CH = topk_chunk_rows(KP);
   P.n_chunks = (T.n + P.CH - 1) / P.CH;
+  P.n_super = (P.n_chunks + TOPK_SUPER - 1) / TOPK_SUPER;
+  // the chunk bound prunes only catalogues larger than the candidate lists (smaller ones are scanned
+  // whole: the lists then hold every dst row, which select's n_dst <= TOPK_KC shortcut relies on)
+  P.prune = tk.prune && T.n > TOPK_KC;
+  std::vector<double> VP;
+  TRYC(topk_dst_basis(c, T, P, VP));
+  HIPCHK(P.d_VP.ensure(VP.size() * 8));
+  HIPCHK(hipMemcpyAsync(P.d_VP.p, VP.data(), VP.size() * 8, hipMemcpyHostToDevice, c->st));
+  const int64_t nn = std::max<int64_t>(T.n, 1);
   HIPCHK(P.d_th.ensure((size_t)std::max<int64_t>(P.n_chunks, 1) * P.CH * KP * 2));
-  HIPCHK(P.d_head.ensure((size_t)std::max<int64_t>(P.n_chunks, 1) * 4));
-  HIPCHK(P.d_keys.ensure((size_t)std::max<int64_t>(T.n, 1) * 8));
-  HIPCHK(P.d_perm.ensure((size_t)std::max<int64_t>(T.n, 1) * 8));
+  HIPCHK(P.d_keys.ensure((size_t)nn * 16));
+  HIPCHK(P.d_perm.ensure((size_t)nn * 8));
+  HIPCHK(P.d_nperm.ensure((size_t)nn * 8));
+  HIPCHK(P.d_tp.ensure((size_t)nn * TOPK_M * 8));
+  HIPCHK(P.d_cfeat.ensure((size_t)std::max<int64_t>(P.n_chunks, 1) * TOPK_CF * 4));
+  HIPCHK(P.d_supf.ensure((size_t)std::max<int64_t>(P.n_super, 1) * TOPK_CF * 4));
+  HIPCHK(P.d_probe.ensure((size_t)256 * KP * 2));
   const size_t tb = topk_sort_temp_bytes(T.n);
   HIPCHK(P.d_tmp.ensure(std::max<size_t>(tb, 16)));
   if (T.n > 0)
-    HIPCHK(topk_prepare(KP, c->p.rank, T.d_orig.as<float>(), T.n, (float)P.tsc, P.d_tmp.p, tb, P.d_keys.as<uint32_t>(),
-                        P.d_perm.as<uint32_t>(), P.d_th.p, P.d_head.as<float>(), c->st));
+    HIPCHK(topk_prepare(KP, c->p.rank, T.d_orig.as<float>(), T.n, (float)P.tsc, P.d_VP.as<double>(), P.d_tmp.p, tb,
+                        P.d_keys.as<uint32_t>(), P.d_perm.as<uint32_t>(), P.d_nperm.as<uint32_t>(),
+                        P.d_tp.as<double>(), P.d_th.p, P.d_cfeat.as<float>(), P.d_supf.as<float>(), P.d_probe.p,
+                        c->st));
   HIPCHK(P.d_dstids.ensure(std::max<int64_t>(T.n, 1) * 4));
   HIPCHK(hipMemcpyAsync(P.d_dstids.p, T.ids.data(), T.n * 4, hipMemcpyHostToDevice, c->st));
   HIPCHK(P.d_scan.ensure(8));
@@ -1541,9 +1582,11 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int3
   a.kt = topk_threshold_rank(k);
   a.tmax_norm = (float)(P.tmax * (1.0 + 1e-6));
   a.Th = P.d_th.p;
-  a.head = P.d_head.as<float>();
   a.perm = P.d_perm.as<uint32_t>();
   a.n_chunks = P.n_chunks;
+  a.VP = P.d_VP.as<double>();
+  a.cfeat = P.prune ? P.d_cfeat.as<float>() : nullptr;
+  a.probe = P.d_probe.p;
   a.ssc = (float)P.ssc;
   a.tsc = (float)P.tsc;
   a.unscale = (float)(1.0 / (P.ssc * P.tsc));
@@ -1563,18 +1606,28 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int3
   // each row's results back to its own slot
   TopkArgs b = a;
   b.drain = tk.drain;
-  if (tk.order) {
-    HIPCHK(P.d_okeys.ensure(nc * 8));
-    HIPCHK(P.d_order.ensure(nc * 8));
-    HIPCHK(P.d_srcs.ensure(nc * 4));
-    const size_t otb = topk_order_temp_bytes(nc);
-    HIPCHK(P.d_otmp.ensure(std::max<size_t>(otb, 16)));
-    HIPCHK(P.d_thr.ensure(nc * 8));
-    HIPCHK(topk_order(KP, a, P.d_otmp.p, otb, P.d_okeys.as<uint32_t>(), P.d_order.as<uint32_t>(),
-                      P.d_srcs.as<int32_t>(), P.d_thr.as<float>(), P.d_thr.as<float>() + nc, c->st));
-    b.src_rows = P.d_srcs.as<int32_t>();
-    b.out_pos = P.d_order.as<uint32_t>();
-    b.thr0 = tk.thr0 ? P.d_thr.as<float>() + nc : nullptr;
+  HIPCHK(P.d_okeys.ensure(nc * 8));
+  HIPCHK(P.d_order.ensure(nc * 8));
+  HIPCHK(P.d_srcs.ensure(nc * 4));
+  const size_t otb = topk_order_temp_bytes(nc);
+  HIPCHK(P.d_otmp.ensure(std::max<size_t>(otb, 16)));
+  HIPCHK(P.d_thr.ensure(nc * 8));
+  HIPCHK(P.d_sf.ensure((size_t)nc * TOPK_SF * 8));
+  float* sf_tmp = P.d_sf.as<float>();
+  float* sf_sorted = sf_tmp + (size_t)nc * TOPK_SF;
+  HIPCHK(topk_order(KP, a, P.d_otmp.p, otb, P.d_okeys.as<uint32_t>(), P.d_order.as<uint32_t>(), P.d_srcs.as<int32_t>(),
+                    P.d_thr.as<float>(), P.d_thr.as<float>() + nc, sf_tmp, sf_sorted, c->st));
+  b.src_rows = P.d_srcs.as<int32_t>();
+  b.out_pos = P.d_order.as<uint32_t>();
+  b.thr0 = tk.thr0 ? P.d_thr.as<float>() + nc : nullptr;
+  b.sfeat = sf_sorted;
+  const int rpw = topk_rows_per_workgroup(KP, nc, c->n_cu);
+  if (P.prune) {  // per scan workgroup, the chunks its rows can need against the starting thresholds
+    const int64_t n_wg = (nc + rpw - 1) / rpw;
+    b.mask_words = (P.n_super + 1) / 2;
+    HIPCHK(P.d_mask.ensure((size_t)n_wg * b.mask_words * 4));
+    b.mask = P.d_mask.as<uint32_t>();
+    HIPCHK(launch_topk_mask(b, rpw, P.d_supf.as<float>(), P.n_super, P.d_mask.as<uint32_t>(), c->st));
   }
   HIPCHK(launch_topk(KP, b, c->n_cu, c->st));
   std::vector<int32_t> need(nc);
@@ -1591,7 +1644,6 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int3
   c->topk_stats[0] += nc;
   c->topk_stats[1] += (int64_t)flagged.size();
   c->topk_stats[2] += (int64_t)scanned;
-  const int rpw = topk_rows_per_workgroup(KP, nc, c->n_cu);
   c->topk_stats[3] += (nc + rpw - 1) / rpw * 4 * P.n_chunks * P.CH;  // dst rows x waves
   if (!flagged.empty()) {
     HIPCHK(P.d_flag.ensure(flagged.size() * 4));

@@ -100,9 +100,15 @@ hipError_t launch_init_random(int KP, int kreal, float* X, int64_t n, uint64_t s
 hipError_t launch_predict(int KP, int kreal, const float* U, const float* V, const int32_t* u,
                           const int32_t* v, float* out, int64_t n, hipStream_t s);
 
-// Top-k (topk.hip): dst rows ordered by descending norm and packed as fp16 (topk_prepare), an MFMA
-// scan with per-row candidate lists and Cauchy-Schwarz early exit, then exact F2J rescoring of the
-// best TOPK_KC candidates with a certification bound (rows that fail it: topk_exact).
+// Top-k (topk.hip): dst rows ordered by descending ‖t_⊥‖ in the dst Gram's eigenbasis and packed as
+// fp16 with per-chunk bound boxes (topk_prepare), a probe pass for the starting thresholds and the src
+// features (topk_order), per-workgroup chunk masks (launch_topk_mask), an MFMA scan over the masked
+// chunks, then exact F2J rescoring of the best TOPK_KC candidates with a certification bound (rows
+// that fail it: topk_exact).
+constexpr int TOPK_M = 4;       // leading eigen-directions of the dst Gram in the pruning bound
+constexpr int TOPK_CF = 12;     // floats per chunk feature record: lo[M], hi[M], R = max ‖t_⊥‖, pad
+constexpr int TOPK_SF = 8;      // floats per src feature record: s_P[M], ‖s_⊥‖, margin, ‖s‖, pad
+constexpr int TOPK_SUPER = 16;  // chunks per super-chunk (mask pre-pass)
 struct TopkArgs {
   const float* S;          // src factors (original basis) [*][KP]
   const float* T;          // dst factors (original basis) [n_dst][KP]
@@ -115,9 +121,14 @@ struct TopkArgs {
   int kt;                  // rank of the running threshold in the candidate lists (k <= kt <= TOPK_KC)
   float tmax_norm;         // max_j ||T_j||_2 (for the error bound)
   const void* Th;          // [n_chunks * chunk rows][KP] fp16: T[perm[p]]·tsc, zero rows past n_dst
-  const float* head;       // [n_chunks] ||T_{perm[c·chunk]}||, rounded up (0 past n_dst)
-  const uint32_t* perm;    // [n_dst] dst row of scan position p (descending norm)
+  const uint32_t* perm;    // [n_dst] dst row of scan position p
   int64_t n_chunks;
+  const double* VP;        // [TOPK_M][KP] leading eigenvectors of the dst Gram (fp64)
+  const float* cfeat;      // [n_chunks][TOPK_CF] chunk bound boxes (null: no pruning)
+  const void* probe;       // [256][KP] fp16 probe rows (the largest norms), ·tsc, zero rows past n_dst
+  const float* sfeat;      // [n_src][TOPK_SF] src features by scan position (order kernel output)
+  const uint32_t* mask;    // [n_wg][mask_words] needed chunks per scan workgroup (null: every chunk)
+  int64_t mask_words;
   float ssc, tsc;          // src / dst fp16 scales (powers of two)
   float unscale;           // 1 / (ssc·tsc): exact rescaling of the MFMA scores
   float scaled;            // ssc·tsc
@@ -134,20 +145,27 @@ struct TopkArgs {
 };
 constexpr int TOPK_KC = 64;     // candidates rescored exactly per src row (k <= 64)
 constexpr int TOPK_CAP = 128;   // candidate list capacity per src row (compacted to 64 above TOPK_TRIG)
-constexpr int TOPK_TRIG = 112;  // compaction trigger: frequent enough that thresholds follow the running 64th best
+constexpr int TOPK_TRIG = 112;  // compaction trigger: frequent enough that thresholds follow the running kt-th best
 constexpr int TOPK_MAX = 512;   // k above TOPK_KC: exact full scan (topk_exact_kernel)
-int topk_chunk_rows(int KP);    // dst rows per scan chunk (Th / head are padded to whole chunks)
+int topk_chunk_rows(int KP);    // dst rows per scan chunk (Th / cfeat are padded to whole chunks)
 size_t topk_sort_temp_bytes(int64_t n_dst);
-// keys: 2·n_dst uint32, perm: 2·n_dst uint32 (perm[0, n_dst) is the result), Th / head as above
-hipError_t topk_prepare(int KP, int kreal, const float* T, int64_t n_dst, float tsc, void* temp, size_t temp_bytes,
-                        uint32_t* keys, uint32_t* perm, void* Th, float* head, hipStream_t s);
+// VP: [TOPK_M][KP] fp64 (device); keys: 4·n uint32, perm / nperm: 2·n uint32 ([0, n) is the result:
+// scan order / descending norm), tp: [n][TOPK_M] fp64 scratch, Th / cfeat / supf (super-chunk boxes)
+// as above, probe: [256][KP] fp16
+hipError_t topk_prepare(int KP, int kreal, const float* T, int64_t n_dst, float tsc, const double* VP, void* temp,
+                        size_t temp_bytes, uint32_t* keys, uint32_t* perm, uint32_t* nperm, double* tp, void* Th,
+                        float* cfeat, float* supf, void* probe, hipStream_t s);
 hipError_t launch_topk(int KP, const TopkArgs& a, int n_cu, hipStream_t s);
-// scan order of the src rows (rows that stop at similar depths share a workgroup): keys / order hold
-// 2·n_src uint32 each; order[0, n_src) = the original position of scan position i, src_sorted[i] =
-// a.src_rows[order[i]] (needs a.S, a.T, a.perm, a.src_rows, a.n_src, a.n_dst)
+// starting thresholds + features + scan order of the src rows: keys / order 2·n_src uint32,
+// thr_tmp / thr_sorted n_src floats, sf_tmp / sf_sorted n_src·TOPK_SF floats
 size_t topk_order_temp_bytes(int64_t n_src);
 hipError_t topk_order(int KP, const TopkArgs& a, void* temp, size_t temp_bytes, uint32_t* keys, uint32_t* order,
-                      int32_t* src_sorted, float* thr_tmp, float* thr_sorted, hipStream_t s);
+                      int32_t* src_sorted, float* thr_tmp, float* thr_sorted, float* sf_tmp, float* sf_sorted,
+                      hipStream_t s);
+// mask[wg][a.mask_words]: the chunks scan workgroup wg (rows_per_wg rows from position wg·rows_per_wg)
+// can need against the starting thresholds (a.thr0, a.sfeat in scan order)
+hipError_t launch_topk_mask(const TopkArgs& a, int rows_per_wg, const float* supf, int64_t n_super, uint32_t* mask,
+                            hipStream_t s);
 int topk_rows_per_workgroup(int KP, int64_t n_src, int n_cu);
 // exact full scan for the given src-row indices (rows == null: rows 0 .. n_rows-1), any k <= TOPK_MAX
 hipError_t launch_topk_exact(int KP, const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s);

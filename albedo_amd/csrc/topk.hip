@@ -2,20 +2,29 @@
 // recommenders/ALSRecommender.scala:28-65: F2J sdot scores, BoundedPriorityQueue top-k,
 // BoundedPriorityQueue.scala:30-53).  The score matrix is never materialised.
 //
-//  prepare  dst rows ordered by descending L2 norm (device radix sort), packed as fp16 rows scaled by
-//           a power of two, plus the norm of every chunk's first row (the largest of that chunk and of
-//           everything after it);
-//  scan     one workgroup per 64·G src rows: the src rows' fp16 fragments stay in registers, the dst
-//           rows stream through an LDS ring filled by LDS-DMA; scores on v_mfma_f32_16x16x32_f16, each
-//           compared with its row's threshold (the 64th best so far) and appended to a per-row list in
-//           global memory; a full list is compacted to its best 64 by a wave bitonic sort.  Because the
-//           dst rows arrive by descending norm, Cauchy-Schwarz ends the scan early: once
-//           ‖s‖·‖t_j‖ <= threshold for every row of the workgroup, no later dst row can enter;
-//  select   one wave per src row: best 64 of the list by approximate score, exact F2J rescoring of
-//           those 64, sort (score desc, id asc), certification: every dst row outside the 64 has
-//           approx <= t (the 64th approx score) or was pruned with ‖s‖‖t_j‖ <= t, so its F2J score is
-//           <= t + e with e the fp16 + fp32 error bound; if the k-th exact score is not > t + e the row
-//           is re-scored by the exact full scan (topk_exact_kernel).
+//  bound    s·t = s_P·t_P + s_⊥·t_⊥ in the eigenbasis of the dst Gram, P = its TOPK_M leading
+//           directions, so s·t <= Σ_d max(s_d·lo_d, s_d·hi_d) + ‖s_⊥‖·R over any set of dst rows whose
+//           t_P lie in the box [lo, hi] and whose ‖t_⊥‖ <= R.  Converged implicit-ALS item factors put
+//           most of their energy in one or two directions (c4: 84 % / 92 %), so the bound is tight:
+//           at c4 it keeps < 1 % of the dst chunks of a user against the 64th best score.
+//  prepare  dst rows by descending ‖t_⊥‖ (device radix sort), packed as fp16 rows scaled by a power of
+//           two, CH-row chunks with their box + R (and 16-chunk super-chunks), a probe image of the 256
+//           largest-norm rows;
+//  order    one wave per 16 src rows: scores against the probe rows on MFMA, the kt-th best v* -> the
+//           starting threshold thr0 = v* minus the rounding difference to the scan; the src features
+//           (s_P, ‖s_⊥‖, the pruning margin); a sort key that groups rows of similar depth;
+//  mask     per scan workgroup, the chunks any of its rows can still need against thr0 (super-chunks
+//           first): a bitmask;
+//  scan     one workgroup per 64·G src rows over the masked chunks: the src rows' fp16 fragments stay in
+//           registers, the dst rows stream through an LDS ring filled by LDS-DMA; a wave skips a chunk
+//           none of its rows can use at the running thresholds; scores on v_mfma_f32_16x16x32_f16
+//           started from minus the thresholds, hits appended to per-row lists in global memory, a
+//           full list compacted to its best 64 by a wave bitonic sort, the kt-th best the new threshold;
+//  select   one wave per src row: best 64 of the list, exact F2J rescoring, sort (score desc, id asc),
+//           certification: every dst row outside the list had approx < its threshold <= t (a pruned
+//           chunk only when bound + e < threshold), so its F2J score is <= t + e with e the fp16 + fp32
+//           error bound; if the k-th exact score is not > t + e the row is re-scored by the exact scan
+//           (topk_exact_kernel, which skips the chunks the bound excludes against its own k-th best).
 // Output is bit-identical to BoundedPriorityQueue over ascending ids + TopByKeyAggregator.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -36,11 +45,15 @@ inline int tk_grid(int64_t n, int per) {
 }
 size_t topk_sort_temp_bytes(int64_t n);
 __global__ void topk_gather_rows_kernel(const int32_t* __restrict__ rows, const float* __restrict__ thr,
-                                        const uint32_t* __restrict__ order, int64_t n, int32_t* __restrict__ out,
-                                        float* __restrict__ thr_out) {
+                                        const float* __restrict__ sf, const uint32_t* __restrict__ order, int64_t n,
+                                        int32_t* __restrict__ out, float* __restrict__ thr_out, float* __restrict__ sf_out) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    out[i] = rows[order[i]];
-    thr_out[i] = thr[order[i]];
+    const uint32_t o = order[i];
+    out[i] = rows[o];
+    thr_out[i] = thr[o];
+#pragma unroll
+    for (int f = 0; f < TOPK_SF; f += 4)
+      *reinterpret_cast<f32x4*>(sf_out + i * TOPK_SF + f) = *reinterpret_cast<const f32x4*>(sf + (int64_t)o * TOPK_SF + f);
   }
 }
 typedef __attribute__((address_space(1))) const void* tk_glb_vp;
@@ -98,9 +111,10 @@ __device__ __forceinline__ void wave_bitonic(float (&sc)[NPL], int (&ix)[NPL]) {
   bitonic_stages<NPL, 2>(sc, ix, threadIdx.x & 63);
 }
 
+
 // ---------------------------------------------------------------------------------------------
-// scan geometry.  A chunk is 16 KiB of fp16 dst rows (128 / 64 / 32 rows at KP = 64 / 128 / 256) plus
-// one 256-B DMA per wave carrying the chunk's head norm; NSTG chunks form the LDS ring.
+// scan geometry.  A chunk is 16 KiB of fp16 dst rows (128 / 64 / 32 rows at KP = 64 / 128 / 256);
+// NSTG chunks form the LDS ring.
 // ---------------------------------------------------------------------------------------------
 template <int KP, int G>
 struct TkScan {
@@ -110,49 +124,24 @@ struct TkScan {
   static constexpr int NJ = CH / 16;             // 16-row tiles per chunk
   static constexpr int NQ = KP / 32;             // 32-deep MFMA steps per tile
   static constexpr int NSTG = G >= 4 ? 6 : 4;    // ring depth (chunks)
-  static constexpr int SLOT = CB + 4 * 256;      // + one norm DMA per wave
+  static constexpr int SLOT = CB;
+  static constexpr int RING = NSTG * SLOT;
   static constexpr int RWG = 64 * G;             // src rows per workgroup (16·G per wave)
   static constexpr int DPW = CB / 1024 / 4;      // 1-KiB row DMAs per wave per chunk
-  static constexpr int NVM = DPW + 1;            // DMA instructions per wave per chunk
-  static constexpr int LDS = NSTG * SLOT + 2 * RWG * 4 + 8 * 4;
+  static constexpr int NVM = DPW;                // DMA instructions per wave per chunk
+  static constexpr int LDS = RING + RWG * 4 + RWG * TOPK_SF * 4;
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
-// Per-wave rings (WV): every wave streams the dst rows through its own 4-deep ring of 8 KiB chunks and
-// runs without workgroup barriers: a wave's list compactions stall only that wave, and each wave
-// stops on its own rows' vote.  Four times the L2 -> LDS traffic of the shared ring.
-template <int KP, int G, bool WV>
-struct TkGeo {
-  static constexpr int RB = 2 * KP;
-  static constexpr int CHP = TkScan<KP, G>::CH;            // rows per prepared chunk (head[] entries)
-  static constexpr int CB = WV ? 8192 : 16384;             // dst bytes per ring chunk
-  static constexpr int CH = CB / RB;
-  static constexpr int NJ = CH / 16;
-  static constexpr int NQ = KP / 32;
-  static constexpr int NSTG = WV ? 4 : TkScan<KP, G>::NSTG;
-  static constexpr int SLOT = CB + (WV ? 256 : 4 * 256);
-  static constexpr int RING = (WV ? 4 : 1) * NSTG * SLOT;  // ring bytes of the workgroup
-  static constexpr int RWG = 64 * G;
-  static constexpr int DPW = WV ? CB / 1024 : CB / 1024 / 4;
-  static constexpr int NVM = DPW + 1;
-  static constexpr int LDS = RING + 2 * RWG * 4 + 8 * 4;
-  static_assert(LDS <= 160 * 1024 && CH % 16 == 0 && CHP % CH == 0, "LDS budget, chunk geometry");
-};
-// 16-B unit u of dst row `row` is stored at unit u ^ tk_sw(row): every ds_read_b128 lane group of a
-// fragment read (16 rows x one unit, cdna ds_read_b128 groups) hits 16 distinct 16-B bank slots.
 template <int KP>
 __host__ __device__ constexpr int topk_chunk_rows_dev() { return TkScan<KP, 2>::CH; }
+// 16-B unit u of dst row `row` is stored at unit u ^ tk_sw(row): every ds_read_b128 lane group of a
+// fragment read (16 rows x one unit, cdna ds_read_b128 groups) hits 16 distinct 16-B bank slots.
 template <int KP>
 __device__ __forceinline__ int tk_sw(int row) {
   if constexpr (KP == 64) return (row >> 1) & 7;
   else return row & 15;
 }
 
-// LDS store the compiler's wait insertion does not see (it would drain the LDS-DMA queue before a
-// plain LDS write); ordered by the explicit lgkmcnt wait ahead of the next barrier
-__device__ __forceinline__ void lds_store_asm(int* p, int v) {
-  const uint32_t addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)p;
-  asm volatile("ds_write_b32 %0, %1" ::"v"(addr), "v"(v) : "memory");
-}
 __device__ __forceinline__ float agent_load(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -160,25 +149,47 @@ __device__ __forceinline__ int agent_load(const int* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int KP, int G, bool WV>
+// Upper bound of s·t over the dst rows of a chunk (or super-chunk) feature record cf = {lo[M], hi[M],
+// R}, for a src row with features sf = {s_P[M], ‖s_⊥‖}; fp32 arithmetic, its rounding is part of the
+// margin stored with the src features (sf[TOPK_M + 1]).
+__device__ __forceinline__ float tk_bound(const float* sf, const float* cf) {
+  float b = sf[TOPK_M] * cf[2 * TOPK_M];
+#pragma unroll
+  for (int d = 0; d < TOPK_M; ++d) b += sf[d] * (sf[d] >= 0.f ? cf[TOPK_M + d] : cf[d]);
+  return b;
+}
+
+// |F2J(s,t) - approx| for the fp16 pre-selection (select's certification bound, see there)
+template <int KP>
+__device__ __forceinline__ double tk_err(double ns, const TopkArgs& a) {
+  const double u = 5.9604644775390625e-08;  // 2^-24
+  const double kk = (double)(KP + 2);
+  const double gam = kk * u / (1.0 - kk * u);
+  const double rel = (9.765625e-04 + 2.384185791015625e-07 + 6.0 * gam) * (1.0 + 1.0 / 512.0);
+  const double tm = (double)a.tmax_norm;
+  const double absu = 2.98023223876953125e-08 * 1.001 * sqrt((double)KP) * (ns / (double)a.tsc + tm / (double)a.ssc) +
+                      (double)KP * 8.9e-16 * (double)a.unscale;
+  return rel * ns * tm + absu;
+}
+
+template <int KP, int G>
 __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
-  using C = TkGeo<KP, G, WV>;
-  constexpr int NQ = C::NQ, NJ = C::NJ, RB = C::RB, CAP = TOPK_CAP;
+  using C = TkScan<KP, G>;
+  constexpr int NQ = C::NQ, NJ = C::NJ, RB = C::RB, CAP = TOPK_CAP, SF = TOPK_SF;
   // a list is compacted to its best 64 once it holds more than TRIG (<= TRIG + 16 <= 64·NSC entries):
-  // frequent enough that the threshold follows the running 64th best
+  // frequent enough that the threshold follows the running kt-th best
   constexpr int TRIG = TOPK_TRIG, NSC = TOPK_CAP / 64;
   static_assert(TRIG + 16 <= 64 * NSC && TRIG + 16 <= CAP && TRIG + 16 <= 255, "compaction width, byte counters");
   extern __shared__ __attribute__((aligned(16))) char lds[];  // one LDS object (glds pipelining)
-  float* s_thr = reinterpret_cast<float*>(lds + C::RING);            // [RWG] thresholds (unscaled)
-  float* s_nrm = s_thr + C::RWG;                                      // [RWG] ‖s‖ rounded up
-  int* s_flag = reinterpret_cast<int*>(s_nrm + C::RWG);           // [2][4] per-wave "done" votes
+  float* s_thr = reinterpret_cast<float*>(lds + C::RING);  // [RWG] thresholds (unscaled)
+  float* s_sf = s_thr + C::RWG;                              // [RWG][SF] src features
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i16 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t rb0 = (int64_t)blockIdx.x * C::RWG;  // first src-list position of the workgroup
   const int wr0 = wave * 16 * G;                     // the wave's first row within the workgroup
   const char* Th = reinterpret_cast<const char*>(a.Th);
-  const int64_t nch = a.n_chunks * (C::CHP / C::CH);
-  char* const ring = lds + (WV ? wave * C::NSTG * C::SLOT : 0);
+  const int64_t nch = a.n_chunks;
+  char* const ring = lds;
 
   // src fragments: lane (i16, g) holds row 16gi + i16, columns 32q + 8g .. +7 (fp16, ·ssc)
   f16x8 sf[G][NQ];
@@ -194,26 +205,18 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
     const int srow = si < a.n_src ? a.src_rows[si] : -1;
     const float* sp = a.S + (int64_t)(srow >= 0 ? srow : 0) * KP + 8 * g;  // loads unconditional (no
     const float keep = srow >= 0 ? 1.f : 0.f;                              // per-element waits)
-    double ss = 0.0;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const f32x4 v0 = ld4(sp + 32 * q), v1 = ld4(sp + 32 * q + 4);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float v = (e < 4 ? v0[e] : v1[e - 4]) * keep;
-        ss += (double)v * (double)v;
-        sf[gi][q][e] = (_Float16)(v * a.ssc);
-      }
+      for (int e = 0; e < 8; ++e) sf[gi][q][e] = (_Float16)((e < 4 ? v0[e] : v1[e - 4]) * keep * a.ssc);
     }
-    ss += __shfl_xor(ss, 16);
-    ss += __shfl_xor(ss, 32);
-    if (g == 0) {
-      const int wrow = wr0 + 16 * gi + i16;
-      s_nrm[wrow] = __double2float_ru(sqrt(ss));
-      s_thr[wrow] = srow < 0 ? INFINITY : (a.thr0 ? a.thr0[si] : -INFINITY);
-    }
+    if (g == 0) s_thr[wr0 + 16 * gi + i16] = srow < 0 ? INFINITY : (a.thr0 ? a.thr0[si] : -INFINITY);
   }
-  if (tid < 8) s_flag[tid] = 0;
+  for (int e = tid; e < C::RWG * SF; e += 256) {
+    const int64_t si = rb0 + e / SF;
+    s_sf[e] = si < a.n_src && a.sfeat ? a.sfeat[rb0 * SF + e] : 0.f;
+  }
   __syncthreads();  // no DMA in flight yet: a plain barrier
   const float tmax_sc = a.tmax_norm * a.tsc;
 #pragma unroll
@@ -225,27 +228,48 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       const int wrow = wr0 + 16 * gi + 4 * g + r;
       const float t0 = s_thr[wrow];
       nthr[gi][r] = t0 == INFINITY ? -INFINITY
-                  : t0 == -INFINITY ? 1.01f * s_nrm[wrow] * a.ssc * tmax_sc + 1.f : -(t0 * a.scaled);
+                  : t0 == -INFINITY ? 1.01f * s_sf[wrow * SF + TOPK_M + 2] * a.ssc * tmax_sc + 1.f : -(t0 * a.scaled);
     }
 
+  // the chunk sequence: the set bits of this workgroup's mask (every chunk without one), ascending
+  const uint32_t* mw = a.mask ? a.mask + (int64_t)blockIdx.x * a.mask_words : nullptr;
+  auto next_chunk = [&](int64_t x) -> int64_t {  // smallest chunk > x in the sequence (nch: none)
+    int64_t c = x + 1;
+    if (!mw) return c < nch ? c : nch;
+    while (c < nch) {
+      const int64_t w = c >> 5;
+      const uint32_t bits = (uint32_t)__builtin_amdgcn_readfirstlane((int)mw[w]) >> (c & 31);
+      if (bits) {
+        c += __builtin_ctz(bits);
+        return c < nch ? c : nch;
+      }
+      c = (w + 1) << 5;
+    }
+    return nch;
+  };
+
   // DMA of chunk c into ring slot `slot`: the wave's DPW KiB of rows (source addresses carry the
-  // unit swizzle, the LDS image is lane-linear), then the chunk's head norm (every lane the same word)
+  // unit swizzle, the LDS image is lane-linear)
   auto dma = [&](int64_t c, int slot) __attribute__((always_inline)) {
     char* base = ring + slot * C::SLOT;
     const int64_t j0 = c * C::CH;
 #pragma unroll
     for (int m = 0; m < C::DPW; ++m) {
-      const int ins = WV ? m : wave * C::DPW + m;
+      const int ins = wave * C::DPW + m;
       const int off = ins * 1024 + 16 * lane;
       const int row = off / RB, up = (off % RB) / 16;
       const char* src = Th + (j0 + row) * RB + 16 * (up ^ tk_sw<KP>(row));
       __builtin_amdgcn_global_load_lds((tk_glb_vp)src, (tk_lds_vp)(base + ins * 1024), 16, 0, 0);
     }
-    __builtin_amdgcn_global_load_lds((tk_glb_vp)(a.head + j0 / C::CHP), (tk_lds_vp)(base + C::CB + (WV ? 0 : wave * 256)),
-                                     4, 0, 0);
   };
-  for (int c = 0; c < C::NSTG - 1; ++c)
-    if (c < nch) dma(c, c);
+  int64_t c_iss = -1, n_iss = 0;
+  for (int u = 0; u < C::NSTG - 1; ++u) {
+    c_iss = next_chunk(c_iss);
+    if (c_iss < nch) {
+      dma(c_iss, u);
+      ++n_iss;
+    }
+  }
 
   // candidates of one 16-row tile (dst positions jt .. jt+15).  Slots come from a ballot prefix count
   // over the 16 lanes of a row's group; list lengths live in registers, one byte per row (cntp[gi]
@@ -338,22 +362,43 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       }
   };
 
-  int64_t c = 0;
-  for (; c < nch; ++c) {
+  int64_t it = 0;
+  for (int64_t c = next_chunk(-1); c < nch; c = next_chunk(c), ++it) {
     // this wave's DMAs of chunk c have landed (in-order VM counter; later list stores only make the
-    // wait stricter), then one barrier publishes every wave's part and retires slot (c-1) % NSTG
-    if (c + C::NSTG - 2 < nch && !a.drain) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NVM * (C::NSTG - 2)) : "memory");
+    // wait stricter), then one barrier publishes every wave's part and retires the previous slot
+    if (n_iss - it - 1 >= C::NSTG - 2 && !a.drain) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NVM * (C::NSTG - 2)) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (!WV) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (c > 0) {
-        const int* fl = s_flag + ((c - 1) & 1) * 4;
-        if (fl[0] & fl[1] & fl[2] & fl[3]) break;  // every row of the workgroup is complete
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (c_iss < nch) {
+      c_iss = next_chunk(c_iss);
+      if (c_iss < nch) {
+        dma(c_iss, (int)((it + C::NSTG - 1) % C::NSTG));
+        ++n_iss;
       }
     }
-    if (c + C::NSTG - 1 < nch) dma(c + C::NSTG - 1, (int)((c + C::NSTG - 1) % C::NSTG));
-    const char* base = ring + (int)(c % C::NSTG) * C::SLOT;
+    // can any row of this wave still take a dst row of chunk c (bound + margin >= its threshold)?
+    bool need = !a.cfeat;
+    if (a.cfeat) {
+      const float* cf = a.cfeat + c * TOPK_CF;
+      float cfr[TOPK_CF];
+#pragma unroll
+      for (int f = 0; f < TOPK_CF; f += 4) {
+        const f32x4 v = ld4(cf + f);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cfr[f + e] = v[e];
+      }
+#pragma unroll
+      for (int h = 0; h < (16 * G + 63) / 64; ++h) {
+        const int rr = lane + 64 * h;
+        if (rr < 16 * G) {
+          const float* srf = s_sf + (wr0 + rr) * SF;
+          need |= tk_bound(srf, cfr) + srf[TOPK_M + 1] >= s_thr[wr0 + rr];
+        }
+      }
+    }
+    if (!__any(need)) continue;
+    const char* base = ring + (int)(it % C::NSTG) * C::SLOT;
     const int64_t j0 = c * C::CH;
     f16x8 df[2][NQ];
     auto rd = [&](int J, f16x8 (&d)[NQ]) __attribute__((always_inline)) {
@@ -376,24 +421,6 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       if constexpr (J > 0) check_tile(acc[(J - 1) & 1], j0 + 16 * (J - 1));
     });
     check_tile(acc[(NJ - 1) & 1], j0 + 16 * (NJ - 1));
-    // vote: every row's threshold already bounds ‖s‖·‖t_j‖ for all j from this chunk on
-    {
-      const float hn = *reinterpret_cast<const float*>(base + C::CB + (WV ? 0 : wave * 256)) * 1.00000095367431640625f;
-      bool ok = true;
-      if (lane < 16 * G) ok = s_nrm[wr0 + lane] * hn <= s_thr[wr0 + lane];
-      if (16 * G > 64) ok = ok && s_nrm[wr0 + 64 + lane] * hn <= s_thr[wr0 + 64 + lane];
-      // no vote before the 256 dst rows behind the starting thresholds are scanned (their 64 best
-      // must reach the lists)
-      const bool done = !__any(!ok) && (c + 1) * C::CH >= 256;
-      if constexpr (WV) {
-        if (done) {
-          ++c;
-          break;
-        }
-      } else {
-        if (lane == 0) lds_store_asm(s_flag + (c & 1) * 4 + wave, done ? 1 : 0);
-      }
-    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup ends
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -406,8 +433,8 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
         if (si < a.n_src) a.lcnt[si] = (int)((cntp[gi] >> (8 * r)) & 0xffu);
       }
   }
-  // dst rows scanned, summed over waves
-  if (a.scanned && (WV ? lane == 0 : tid == 0)) atomicAdd(a.scanned, (unsigned long long)(c * C::CH * (WV ? 1 : 4)));
+  // dst rows streamed by the workgroup (chunks x rows x 4 waves, the full-scan unit of topk_stats)
+  if (a.scanned && tid == 0) atomicAdd(a.scanned, (unsigned long long)(it * C::CH * 4));
 }
 
 // One wave per src row: best 64 of the list, exact F2J rescoring, sort, certify, write top-k.
@@ -454,8 +481,8 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
     const double absu = 2.98023223876953125e-08 * 1.001 * sqrt((double)KP) *
                         (ns / (double)a.tsc + tm / (double)a.ssc) + (double)KP * 8.9e-16 * (double)a.unscale;
     const double e = rel * ns * tm + absu;
-    // fewer than 64 listed (a scan that stopped before 64 rows reached a starting threshold): the
-    // bound below needs t >= the last threshold, which only a full list guarantees
+    // fewer than kt listed: the bound below needs t >= every threshold the scan used, which only a
+    // list of kt entries guarantees
     if (cnt < a.kt || !((double)kth > (double)t + e)) {
       if (lane == 0) a.need_exact[so] = 1;
     }
@@ -467,18 +494,21 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
   }
 }
 
-// Scan order and starting thresholds of the src rows.  A workgroup's scan ends when its slowest row
-// can stop, so rows that stop at similar depths go together.  One wave per 16 src rows scores them
-// against the 256 largest-norm dst rows with the scan's own fp16 operands on MFMA, and v* = the
-// 64th best of those 256 (bisection on order-preserving keys): a lower bound of the row's final
-// 64th best.  thr0 = v* minus the
-// rounding difference between this accumulation and the scan's (8γ_{KP+2}·‖s‖·max‖t‖) is a valid
-// starting threshold: the 64 dst rows above v* reach the list, so the final 64th approximate score
-// is >= thr0.  key = thr0 / ‖s‖: the row can stop once ‖t_j‖ <= threshold / ‖s‖, so a larger key
-// stops earlier (order-preserving uint of the float, sorted descending with the positions as values).
+
+// Scan order, starting thresholds and features of the src rows.  One wave per 16 src rows scores them
+// against the probe rows (the 256 largest-norm dst rows, fp16 like the scan) on MFMA and finds each
+// row's exact kt-th best v* of those 256 by bisection on order-preserving keys.  thr0 = v* minus the
+// accumulation difference between this pass and the scan (8γ_{KP+2}·‖s‖·max‖t‖) is a valid starting
+// threshold: the probe rows above v* reach the list (their chunks' bound is >= their score), so the
+// final kt-th approximate score is >= thr0.  Features (TOPK_SF floats): s_P (fp64 dots with the
+// dst Gram's leading eigenvectors, rounded), ‖s_⊥‖ (rounded up, with a floor for the fp64 cancellation),
+// the pruning margin e + 1.2e-5·‖s‖·max‖t‖ (e: select's approx error; 1.2e-5 covers the fp32 bound
+// arithmetic and F2J's own rounding), ‖s‖ rounded up.  Sort key: thr0 / ‖s‖ (rows that stop at
+// similar depths share a workgroup).
 template <int KP>
 __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_t* __restrict__ key,
-                                                             uint32_t* __restrict__ val, float* __restrict__ thr0) {
+                                                             uint32_t* __restrict__ val, float* __restrict__ thr0,
+                                                             float* __restrict__ sfo) {
   constexpr int NQ = KP / 32, RB = 2 * KP;
   const int lane = threadIdx.x & 63, g = lane >> 4, i16 = lane & 15;
   const int64_t sb = (int64_t)blockIdx.x * 64 + (threadIdx.x >> 6) * 16;  // the wave's first position
@@ -487,21 +517,29 @@ __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_
   const float* sp = a.S + (int64_t)(srow >= 0 ? srow : 0) * KP + 8 * g;
   const float keep = srow >= 0 ? 1.f : 0.f;
   f16x8 sf[NQ];
-  double ss = 0.0;
+  double ss = 0.0, spd[TOPK_M] = {};
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const f32x4 v0 = ld4(sp + 32 * q), v1 = ld4(sp + 32 * q + 4);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float v = (e < 4 ? v0[e] : v1[e - 4]) * keep;
+      const int col = 32 * q + 8 * g + e;
       ss += (double)v * (double)v;
+#pragma unroll
+      for (int d = 0; d < TOPK_M; ++d) spd[d] += (double)v * a.VP[d * KP + col];
       sf[q][e] = (_Float16)(v * a.ssc);
     }
   }
   ss += __shfl_xor(ss, 16);
   ss += __shfl_xor(ss, 32);  // every lane: ‖s‖² of row i16
-  const char* Th = reinterpret_cast<const char*>(a.Th);
-  const int64_t n_pad = a.n_chunks * (int64_t)topk_chunk_rows_dev<KP>();
+#pragma unroll
+  for (int d = 0; d < TOPK_M; ++d) {
+    spd[d] += __shfl_xor(spd[d], 16);
+    spd[d] += __shfl_xor(spd[d], 32);
+  }
+  const char* Pr = reinterpret_cast<const char*>(a.probe);
+  const int64_t n_probe = a.n_dst < 256 ? a.n_dst : 256;
   // order-preserving uint keys of the 256 scores: lane (i16, g) holds column 16J + i16 of rows 4g + r
   uint32_t u[16][4];
 #pragma unroll
@@ -510,17 +548,16 @@ __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_
     f32x4 acc = zero4();
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      f16x8 d = {};
-      if (p < n_pad) d = *reinterpret_cast<const f16x8*>(Th + p * RB + 16 * (4 * q + g));
+      const f16x8 d = *reinterpret_cast<const f16x8*>(Pr + p * RB + 16 * (4 * q + g));  // zero rows past n
       acc = mfma_h(sf[q], d, acc);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const uint32_t bb = __float_as_uint(p < a.n_dst ? acc[r] : -INFINITY);
+      const uint32_t bb = __float_as_uint(p < n_probe ? acc[r] : -INFINITY);
       u[J][r] = (bb & 0x80000000u) ? ~bb : (bb | 0x80000000u);
     }
   }
-  // exact 64th largest per row: bisection on the key (count of keys >= mid over the row's 16 lanes)
+  // exact kt-th largest per row: bisection on the key (count of keys >= mid over the row's 16 lanes)
   float vs[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -536,7 +573,16 @@ __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_
     }
     vs[r] = __uint_as_float((lo & 0x80000000u) ? (lo & 0x7fffffffu) : ~lo);
   }
-  const double nrm = sqrt(__shfl(ss, 4 * g + (i16 & 3)));  // ‖s‖ of row 4g + r (all lanes take part)
+  const int rsel = 4 * g + (i16 & 3);  // the row this lane reports in the group (lanes i16 < 4)
+  const double nrm2 = __shfl(ss, rsel);
+  const double nrm = sqrt(nrm2);
+  double sq[TOPK_M];
+  double pp = 0.0;
+#pragma unroll
+  for (int d = 0; d < TOPK_M; ++d) {
+    sq[d] = __shfl(spd[d], rsel);
+    pp += sq[d] * sq[d];
+  }
   if (i16 < 4) {
     const int r = i16;
     const int64_t pr = sb + 4 * g + r;
@@ -552,32 +598,105 @@ __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_
       const uint32_t bb = __float_as_uint(k);
       key[pr] = (bb & 0x80000000u) ? ~bb : (bb | 0x80000000u);
       val[pr] = (uint32_t)pr;
+      float* o = sfo + pr * TOPK_SF;
+#pragma unroll
+      for (int d = 0; d < TOPK_M; ++d) o[d] = (float)sq[d];
+      o[TOPK_M] = __double2float_ru(sqrt(fmax(nrm2 - pp, 0.0) + 1e-13 * nrm2));
+      o[TOPK_M + 1] = (float)(tk_err<KP>(nrm, a) + 1.2e-5 * nrm * (double)a.tmax_norm) * 1.0001f;
+      o[TOPK_M + 2] = __double2float_ru(nrm);
+      o[TOPK_M + 3] = 0.f;
     }
   }
 }
 
 size_t topk_order_temp_bytes(int64_t n_src) { return topk_sort_temp_bytes(n_src); }
 
-// src_sorted[i] = src_rows[order[i]], thr_sorted[i] = thr0[order[i]]; order[i] = the position whose
-// results slot i fills
+// src_sorted[i] = src_rows[order[i]] (and thr0, features); order[i] = the position whose results
+// slot i fills
 hipError_t topk_order(int KP, const TopkArgs& a, void* temp, size_t temp_bytes, uint32_t* keys, uint32_t* order,
-                      int32_t* src_sorted, float* thr_tmp, float* thr_sorted, hipStream_t s) {
+                      int32_t* src_sorted, float* thr_tmp, float* thr_sorted, float* sf_tmp, float* sf_sorted,
+                      hipStream_t s) {
   const int64_t n = a.n_src;
   if (n <= 0) return hipSuccess;
   uint32_t* k0 = keys;
   uint32_t* k1 = keys + n;
   uint32_t* v0 = order + n;
   const int blocks = (int)((n + 63) / 64);
-  if (KP == 64) topk_order_key_kernel<64><<<blocks, 256, 0, s>>>(a, k0, v0, thr_tmp);
-  else if (KP == 128) topk_order_key_kernel<128><<<blocks, 256, 0, s>>>(a, k0, v0, thr_tmp);
-  else topk_order_key_kernel<256><<<blocks, 256, 0, s>>>(a, k0, v0, thr_tmp);
+  if (KP == 64) topk_order_key_kernel<64><<<blocks, 256, 0, s>>>(a, k0, v0, thr_tmp, sf_tmp);
+  else if (KP == 128) topk_order_key_kernel<128><<<blocks, 256, 0, s>>>(a, k0, v0, thr_tmp, sf_tmp);
+  else topk_order_key_kernel<256><<<blocks, 256, 0, s>>>(a, k0, v0, thr_tmp, sf_tmp);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   size_t tb = temp_bytes;
   e = rocprim::radix_sort_pairs_desc(temp, tb, k0, k1, v0, order, (size_t)n, 0, 32, s);
   if (e != hipSuccess) return e;
-  topk_gather_rows_kernel<<<tk_grid(n, 256), 256, 0, s>>>(a.src_rows, thr_tmp, order, n, src_sorted, thr_sorted);
+  topk_gather_rows_kernel<<<tk_grid(n, 256), 256, 0, s>>>(a.src_rows, thr_tmp, sf_tmp, order, n, src_sorted,
+                                                          thr_sorted, sf_sorted);
   return hipGetLastError();
+}
+
+// The chunks each scan workgroup can need: chunk c is needed when some row i of the workgroup has
+// bound(s_i, c) + margin_i >= thr0_i; rows of a chunk that is not needed have approx < thr0 <= every
+// threshold the scan will use, so the scan would not append any of them.  Super-chunks (16 chunks,
+// the union box) are tested first.  One bit per chunk: word w holds chunks 32w .. 32w+31 (super-chunks
+// 2w and 2w + 1).
+__global__ __launch_bounds__(256) void topk_mask_kernel(TopkArgs a, int rwg, const float* __restrict__ supf,
+                                                        int64_t n_super, uint32_t* __restrict__ mask) {
+  extern __shared__ __attribute__((aligned(16))) float rf[];  // [rwg][8]: s_P, ‖s_⊥‖, thr0 - margin
+  __shared__ uint16_t ms[4096];                              // one batch of super-chunk masks
+  const int tid = threadIdx.x;
+  const int64_t p0 = (int64_t)blockIdx.x * rwg;
+  int nrow = 0;
+  for (int i = tid; i < rwg; i += 256) {
+    const int64_t p = p0 + i;
+    float* o = rf + 8 * i;
+    if (p < a.n_src) {
+      const float* f = a.sfeat + p * TOPK_SF;
+#pragma unroll
+      for (int d = 0; d <= TOPK_M; ++d) o[d] = f[d];
+      const float t0 = a.thr0 ? a.thr0[p] : -INFINITY;
+      o[TOPK_M + 1] = t0 == -INFINITY ? -INFINITY : t0 - f[TOPK_M + 1];
+    } else {
+#pragma unroll
+      for (int d = 0; d <= TOPK_M; ++d) o[d] = 0.f;
+      o[TOPK_M + 1] = INFINITY;
+    }
+  }
+  nrow = (int)std::min<int64_t>(rwg, a.n_src - p0);
+  __syncthreads();
+  auto needed = [&](const float* cf) {
+    float c[TOPK_CF];
+#pragma unroll
+    for (int f = 0; f < TOPK_CF; f += 4) {
+      const f32x4 v = ld4(cf + f);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) c[f + e] = v[e];
+    }
+    for (int i = 0; i < nrow; ++i)
+      if (tk_bound(rf + 8 * i, c) >= rf[8 * i + TOPK_M + 1]) return true;
+    return false;
+  };
+  uint32_t* mrow = mask + (int64_t)blockIdx.x * a.mask_words;
+  for (int64_t s0 = 0; s0 < n_super; s0 += 4096) {
+    const int nb = (int)std::min<int64_t>(4096, n_super - s0);
+    for (int j = tid; j < nb; j += 256) {
+      const int64_t sup = s0 + j;
+      uint32_t bits = 0u;
+      if (needed(supf + sup * TOPK_CF)) {
+        for (int c = 0; c < TOPK_SUPER; ++c) {
+          const int64_t ch = sup * TOPK_SUPER + c;
+          if (ch < a.n_chunks && needed(a.cfeat + ch * TOPK_CF)) bits |= 1u << c;
+        }
+      }
+      ms[j] = (uint16_t)bits;
+    }
+    __syncthreads();
+    for (int w = tid; w < (nb + 1) / 2; w += 256) {
+      const uint32_t lo = ms[2 * w], hi = 2 * w + 1 < nb ? ms[2 * w + 1] : 0u;
+      mrow[s0 / 2 + w] = lo | (hi << 16);
+    }
+    __syncthreads();
+  }
 }
 
 // Exact path: one workgroup (4 waves) per src row, full F2J scan.  Each wave keeps its best 64·P
@@ -585,7 +704,9 @@ hipError_t topk_order(int KP, const TopkArgs& a, void* temp, size_t temp_bytes, 
 // [P, 2P); a batch of 64 scores is only buffered when one of them reaches the current 64·P-th best,
 // and a full buffer is merged by one bitonic sort of the 128·P slots.  The four waves' lists are
 // merged at the end.  P = 1 serves the rows the MFMA pre-selection could not certify; P up to 8
-// serves k up to 512 (recommendForAll* with k > 64, no pre-selection).
+// serves k up to 512 (recommendForAll* with k > 64, no pre-selection).  The dst rows are visited in
+// the prepared chunk order and a chunk whose bound (+ F2J rounding) is below the wave's own 64·P-th
+// best is skipped: none of its rows can enter the merged top-k (<= 64·P), ties included.
 template <int KP, int P>
 __global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32_t* rows, int64_t row0) {
   __shared__ float msc[4][64 * P];
@@ -600,19 +721,38 @@ __global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32
   for (int h = 0; h < 2 * P; ++h) { bs[h] = -INFINITY; bi[h] = -1; }
   int nin = 0;                // newcomer batches buffered (wave-uniform)
   float thr = -INFINITY;      // the kept list's last score once full
-  // with the prepared norm order (a.perm / a.head) dst rows are visited by descending norm and a wave
-  // stops once ‖s‖·‖t_j‖ bounds every later F2J score below its own 64·P-th best (which is <= the
-  // merged k-th): F2J(s, t) <= ‖s‖‖t‖(1 + (KP+2)·2^-24), covered by the 2^-14 factor
-  float snrm = 0.f;
-  if (a.perm) {
-    double nn = 0.0;
-    for (int c = lane; c < a.kreal; c += 64) nn += (double)s[c] * (double)s[c];
-    for (int o = 32; o > 0; o >>= 1) nn += __shfl_xor(nn, o);
-    snrm = __double2float_ru(sqrt(nn)) * 1.00006103515625f;
+  // this row's bound features (fp64, like the order kernel's)
+  float sfe[TOPK_M + 1];
+  float marg = 0.f;
+  if (a.cfeat) {
+    double nn = 0.0, sp[TOPK_M] = {};
+    for (int c = lane; c < a.kreal; c += 64) {
+      const double v = (double)s[c];
+      nn += v * v;
+#pragma unroll
+      for (int d = 0; d < TOPK_M; ++d) sp[d] += v * a.VP[d * KP + c];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      nn += __shfl_xor(nn, o);
+#pragma unroll
+      for (int d = 0; d < TOPK_M; ++d) sp[d] += __shfl_xor(sp[d], o);
+    }
+    double pp = 0.0;
+#pragma unroll
+    for (int d = 0; d < TOPK_M; ++d) {
+      sfe[d] = (float)sp[d];
+      pp += sp[d] * sp[d];
+    }
+    sfe[TOPK_M] = __double2float_ru(sqrt(fmax(nn - pp, 0.0) + 1e-13 * nn));
+    marg = (float)(1.2e-5 * sqrt(nn) * (double)a.tmax_norm) * 1.0001f + 1e-30f;
   }
   const int ch = topk_chunk_rows_dev<KP>();
   for (int64_t j0 = (int64_t)wave * 64; j0 < a.n_dst; j0 += 256) {
-    if (a.perm && thr > -INFINITY && snrm * a.head[j0 / ch] < thr) break;
+    if (a.cfeat && thr > -INFINITY) {
+      float b = -INFINITY;
+      for (int64_t c = j0 / ch; c <= (j0 + 63) / ch && c < a.n_chunks; ++c) b = fmaxf(b, tk_bound(sfe, a.cfeat + c * TOPK_CF));
+      if (b + marg < thr) continue;
+    }
     const int64_t pj = j0 + lane;
     const int64_t dj = (a.perm && pj < a.n_dst) ? (int64_t)a.perm[pj] : pj;
     const float sc = pj < a.n_dst ? f2j_dot_v4(s, a.T + dj * KP, a.kreal) : -INFINITY;
@@ -657,30 +797,113 @@ __global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32
 // ---------------------------------------------------------------------------------------------
 // preparation of the dst side
 // ---------------------------------------------------------------------------------------------
-// key[j] = bits of ‖T_j‖ rounded up to fp32 (non-negative floats order as unsigned), val[j] = j
-__global__ void topk_norm_keys_kernel(const float* __restrict__ T, int64_t n, int KP, int kreal,
-                                      uint32_t* __restrict__ key, uint32_t* __restrict__ val) {
+// per dst row r (one wave): t_P (fp64) = VP·t, pkey = bits of ‖t_⊥‖ rounded up (with a floor for the
+// fp64 cancellation), nkey = bits of ‖t‖ rounded up; vals = r for both sorts
+__global__ void topk_feat_kernel(const float* __restrict__ T, int64_t n, int KP, int kreal, const double* __restrict__ VP,
+                                 double* __restrict__ tp, uint32_t* __restrict__ pkey, uint32_t* __restrict__ pval,
+                                 uint32_t* __restrict__ nkey, uint32_t* __restrict__ nval) {
   const int lane = threadIdx.x & 63;
   for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += (int64_t)gridDim.x * 4) {
-    double s2 = 0.0;
-    for (int c = lane; c < kreal; c += 64) s2 += (double)T[r * KP + c] * (double)T[r * KP + c];
-    for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
+    double s2 = 0.0, sp[TOPK_M] = {};
+    for (int c = lane; c < kreal; c += 64) {
+      const double v = (double)T[r * KP + c];
+      s2 += v * v;
+#pragma unroll
+      for (int d = 0; d < TOPK_M; ++d) sp[d] += v * VP[d * KP + c];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      s2 += __shfl_xor(s2, o);
+#pragma unroll
+      for (int d = 0; d < TOPK_M; ++d) sp[d] += __shfl_xor(sp[d], o);
+    }
     if (lane == 0) {
-      key[r] = __float_as_uint(__double2float_ru(sqrt(s2)));
-      val[r] = (uint32_t)r;
+      double pp = 0.0;
+#pragma unroll
+      for (int d = 0; d < TOPK_M; ++d) {
+        tp[r * TOPK_M + d] = sp[d];
+        pp += sp[d] * sp[d];
+      }
+      pkey[r] = __float_as_uint(__double2float_ru(sqrt(fmax(s2 - pp, 0.0) + 1e-13 * s2)));
+      pval[r] = (uint32_t)r;
+      nkey[r] = __float_as_uint(__double2float_ru(sqrt(s2)));
+      nval[r] = (uint32_t)r;
     }
   }
 }
-// Th[p] = fp16(T[perm[p]]·tsc) (zero rows past n), head[c] = ‖T_{perm[c·CH]}‖ (0 past n)
+// Th[p] = fp16(T[perm[p]]·tsc) (zero rows past n)
 __global__ void topk_pack_kernel(const float* __restrict__ T, int64_t n, int64_t n_pad, int KP, float tsc,
-                                 const uint32_t* __restrict__ perm, const uint32_t* __restrict__ skey, int CH,
-                                 _Float16* __restrict__ Th, float* __restrict__ head) {
+                                 const uint32_t* __restrict__ perm, _Float16* __restrict__ Th) {
   const int64_t tot = n_pad * KP;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t p = e / KP;
     const int c = (int)(e % KP);
     Th[e] = p < n ? (_Float16)(T[(int64_t)perm[p] * KP + c] * tsc) : (_Float16)0.f;
-    if (c == 0 && p % CH == 0) head[p / CH] = p < n ? __uint_as_float(skey[p]) : 0.f;
+  }
+}
+// chunk c (one wave): box of t_P over its rows (fp64, rounded outward) and R = max ‖t_⊥‖ (sorted keys)
+__global__ void topk_chunk_feat_kernel(const double* __restrict__ tp, const uint32_t* __restrict__ perm,
+                                       const uint32_t* __restrict__ pkey_sorted, int64_t n, int CH, int64_t n_chunks,
+                                       float* __restrict__ cfeat) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < n_chunks; c += (int64_t)gridDim.x * 4) {
+    double lo[TOPK_M], hi[TOPK_M];
+#pragma unroll
+    for (int d = 0; d < TOPK_M; ++d) { lo[d] = INFINITY; hi[d] = -INFINITY; }
+    float R = 0.f;
+    for (int j = lane; j < CH; j += 64) {
+      const int64_t p = c * CH + j;
+      if (p < n) {
+        const uint32_t r = perm[p];
+#pragma unroll
+        for (int d = 0; d < TOPK_M; ++d) {
+          const double v = tp[(int64_t)r * TOPK_M + d];
+          lo[d] = fmin(lo[d], v);
+          hi[d] = fmax(hi[d], v);
+        }
+        R = fmaxf(R, __uint_as_float(pkey_sorted[p]));
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+      for (int d = 0; d < TOPK_M; ++d) {
+        lo[d] = fmin(lo[d], __shfl_xor(lo[d], o));
+        hi[d] = fmax(hi[d], __shfl_xor(hi[d], o));
+      }
+      R = fmaxf(R, __shfl_xor(R, o));
+    }
+    if (lane == 0) {
+      float* o = cfeat + c * TOPK_CF;
+#pragma unroll
+      for (int d = 0; d < TOPK_M; ++d) {
+        o[d] = lo[d] == INFINITY ? 0.f : __double2float_rd(lo[d]);
+        o[TOPK_M + d] = hi[d] == -INFINITY ? 0.f : __double2float_ru(hi[d]);
+      }
+      o[2 * TOPK_M] = R;
+      for (int f = 2 * TOPK_M + 1; f < TOPK_CF; ++f) o[f] = 0.f;
+    }
+  }
+}
+// super-chunk s: the union of its TOPK_SUPER chunk boxes
+__global__ void topk_super_feat_kernel(const float* __restrict__ cfeat, int64_t n_chunks, int64_t n_super,
+                                       float* __restrict__ supf) {
+  for (int64_t sidx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; sidx < n_super; sidx += (int64_t)gridDim.x * blockDim.x) {
+    float o[TOPK_CF];
+#pragma unroll
+    for (int d = 0; d < TOPK_M; ++d) { o[d] = INFINITY; o[TOPK_M + d] = -INFINITY; }
+    o[2 * TOPK_M] = 0.f;
+    for (int c = 0; c < TOPK_SUPER; ++c) {
+      const int64_t ch = sidx * TOPK_SUPER + c;
+      if (ch >= n_chunks) break;
+      const float* f = cfeat + ch * TOPK_CF;
+#pragma unroll
+      for (int d = 0; d < TOPK_M; ++d) {
+        o[d] = fminf(o[d], f[d]);
+        o[TOPK_M + d] = fmaxf(o[TOPK_M + d], f[TOPK_M + d]);
+      }
+      o[2 * TOPK_M] = fmaxf(o[2 * TOPK_M], f[2 * TOPK_M]);
+    }
+    for (int f = 2 * TOPK_M + 1; f < TOPK_CF; ++f) o[f] = 0.f;
+    for (int f = 0; f < TOPK_CF; ++f) supf[sidx * TOPK_CF + f] = o[f];
   }
 }
 
@@ -700,41 +923,47 @@ size_t topk_sort_temp_bytes(int64_t n) {
   return tb;
 }
 
-hipError_t topk_prepare(int KP, int kreal, const float* T, int64_t n, float tsc, void* temp, size_t temp_bytes,
-                        uint32_t* keys, uint32_t* perm, void* Th, float* head, hipStream_t s) {
+hipError_t topk_prepare(int KP, int kreal, const float* T, int64_t n, float tsc, const double* VP, void* temp,
+                        size_t temp_bytes, uint32_t* keys, uint32_t* perm, uint32_t* nperm, double* tp, void* Th,
+                        float* cfeat, float* supf, void* probe, hipStream_t s) {
   const int CH = topk_chunk_rows(KP);
-  const int64_t n_pad = (n + CH - 1) / CH * CH;
-  uint32_t* k0 = keys;
-  uint32_t* k1 = keys + n;
-  uint32_t* v0 = perm + n;  // perm has 2n slots: [n, 2n) holds the unsorted values
-  topk_norm_keys_kernel<<<tk_grid(n, 4), 256, 0, s>>>(T, n, KP, kreal, k0, v0);
+  const int64_t n_pad = (n + CH - 1) / CH * CH, n_chunks = n_pad / CH;
+  const int64_t n_super = (n_chunks + TOPK_SUPER - 1) / TOPK_SUPER;
+  uint32_t* pk0 = keys;          // ‖t_⊥‖ keys, unsorted / sorted
+  uint32_t* pk1 = keys + n;
+  uint32_t* nk0 = keys + 2 * n;  // ‖t‖ keys
+  uint32_t* nk1 = keys + 3 * n;
+  topk_feat_kernel<<<tk_grid(n, 4), 256, 0, s>>>(T, n, KP, kreal, VP, tp, pk0, perm + n, nk0, nperm + n);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   size_t tb = temp_bytes;
-  e = rocprim::radix_sort_pairs_desc(temp, tb, k0, k1, v0, perm, (size_t)n, 0, 32, s);
+  e = rocprim::radix_sort_pairs_desc(temp, tb, pk0, pk1, perm + n, perm, (size_t)n, 0, 32, s);
   if (e != hipSuccess) return e;
-  topk_pack_kernel<<<tk_grid(n_pad * KP, 256), 256, 0, s>>>(T, n, n_pad, KP, tsc, perm, k1, CH,
-                                                            reinterpret_cast<_Float16*>(Th), head);
+  tb = temp_bytes;
+  e = rocprim::radix_sort_pairs_desc(temp, tb, nk0, nk1, nperm + n, nperm, (size_t)n, 0, 32, s);
+  if (e != hipSuccess) return e;
+  topk_pack_kernel<<<tk_grid(n_pad * KP, 256), 256, 0, s>>>(T, n, n_pad, KP, tsc, perm, reinterpret_cast<_Float16*>(Th));
+  topk_pack_kernel<<<tk_grid(256 * KP, 256), 256, 0, s>>>(T, std::min<int64_t>(n, 256), 256, KP, tsc, nperm,
+                                                          reinterpret_cast<_Float16*>(probe));
+  topk_chunk_feat_kernel<<<tk_grid(n_chunks, 4), 256, 0, s>>>(tp, perm, pk1, n, CH, n_chunks, cfeat);
+  topk_super_feat_kernel<<<tk_grid(n_super, 256), 256, 0, s>>>(cfeat, n_chunks, n_super, supf);
+  return hipGetLastError();
+}
+
+hipError_t launch_topk_mask(const TopkArgs& a, int rows_per_wg, const float* supf, int64_t n_super, uint32_t* mask,
+                            hipStream_t s) {
+  const int64_t n_wg = (a.n_src + rows_per_wg - 1) / rows_per_wg;
+  if (n_wg <= 0) return hipSuccess;
+  topk_mask_kernel<<<(int)n_wg, 256, (size_t)rows_per_wg * 8 * 4, s>>>(a, rows_per_wg, supf, n_super, mask);
   return hipGetLastError();
 }
 
 template <int KP, int G>
 hipError_t launch_scan(const TopkArgs& a, hipStream_t s) {
-  // default: one ring per workgroup; "wave": per-wave rings (measured 2.69 s vs 2.60 s at c4: the
-  // waves of a workgroup stop together, so the barriers cost little and the 4x ring traffic shows)
-  static const char* ev = std::getenv("ALBEDO_TOPK_SCAN");
-  const bool wv = ev && std::string(ev) == "wave";
-  if (wv) {
-    using C = TkGeo<KP, G, true>;
-    static const hipError_t attr = allow_lds(topk_scan_kernel<KP, G, true>, C::LDS);
-    if (attr != hipSuccess) return attr;
-    topk_scan_kernel<KP, G, true><<<(int)((a.n_src + C::RWG - 1) / C::RWG), 256, C::LDS, s>>>(a);
-  } else {
-    using C = TkGeo<KP, G, false>;
-    static const hipError_t attr = allow_lds(topk_scan_kernel<KP, G, false>, C::LDS);
-    if (attr != hipSuccess) return attr;
-    topk_scan_kernel<KP, G, false><<<(int)((a.n_src + C::RWG - 1) / C::RWG), 256, C::LDS, s>>>(a);
-  }
+  using C = TkScan<KP, G>;
+  static const hipError_t attr = allow_lds(topk_scan_kernel<KP, G>, C::LDS);
+  if (attr != hipSuccess) return attr;
+  topk_scan_kernel<KP, G><<<(int)((a.n_src + C::RWG - 1) / C::RWG), 256, C::LDS, s>>>(a);
   return hipGetLastError();
 }
 
