@@ -1446,7 +1446,7 @@ struct TopkPlan {
   int64_t n_chunks = 0, n_super = 0;
   bool prune = false;
   DevBuf d_th, d_keys, d_perm, d_nperm, d_tp, d_tmp, d_dstids, d_VP, d_cfeat, d_supf, d_probe, d_slab, d_G;
-  DevBuf d_src, d_ls, d_li, d_lc, d_need, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp, d_thr, d_sf, d_mask;
+  DevBuf d_src, d_ls, d_li, d_lc, d_need, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp, d_thr, d_sf, d_mask, d_kth;
 };
 
 // The leading TOPK_M eigenvectors of the dst side's Gram Σ t tᵀ (original basis), fp64 [TOPK_M][KP]:
@@ -1597,6 +1597,10 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int3
   a.out_ids = d_oid;
   a.out_scores = d_osc;
   a.need_exact = P.d_need.as<int32_t>();
+  if (!P.exact_only) {
+    HIPCHK(P.d_kth.ensure(nc * 4));
+    a.kth0 = P.d_kth.as<float>();
+  }
   a.scanned = P.d_scan.as<unsigned long long>();
   if (P.exact_only) {
     HIPCHK(launch_topk_exact(KP, a, nullptr, nc, c->st));

@@ -138,6 +138,7 @@ struct TopkArgs {
   int32_t* out_ids;        // [n_src][k] raw dst ids
   float* out_scores;       // [n_src][k]
   int32_t* need_exact;     // [n_src] set when the candidate set could not be certified
+  float* kth0;             // [n_src] select -> exact rescan: the certification pass's k-th exact score (or null)
   unsigned long long* scanned;  // += dst chunks scanned by each scan workgroup (or null)
   const uint32_t* out_pos;      // select: results of scan position i go to slot out_pos[i] (or i)
   const float* thr0;            // scan: starting threshold of each src position (topk_order; or null)

@@ -124,12 +124,13 @@ struct TkScan {
   static constexpr int NJ = CH / 16;             // 16-row tiles per chunk
   static constexpr int NQ = KP / 32;             // 32-deep MFMA steps per tile
   static constexpr int NSTG = G >= 4 ? 6 : 4;    // ring depth (chunks)
-  static constexpr int SLOT = CB;
+  static constexpr int SLOT = CB + 4 * 64;       // + each wave's copy of the chunk's bound box
   static constexpr int RING = NSTG * SLOT;
   static constexpr int RWG = 64 * G;             // src rows per workgroup (16·G per wave)
   static constexpr int DPW = CB / 1024 / 4;      // 1-KiB row DMAs per wave per chunk
-  static constexpr int NVM = DPW;                // DMA instructions per wave per chunk
-  static constexpr int LDS = RING + RWG * 4 + RWG * TOPK_SF * 4;
+  static constexpr int NVM = DPW + 1;            // DMA instructions per wave per chunk (rows + box)
+  static constexpr int MASKW = 8192;             // mask words kept in LDS (chunks 0 .. 262143)
+  static constexpr int LDS = RING + RWG * 4 + RWG * TOPK_SF * 4 + MASKW * 4;
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 template <int KP>
@@ -183,6 +184,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];  // one LDS object (glds pipelining)
   float* s_thr = reinterpret_cast<float*>(lds + C::RING);  // [RWG] thresholds (unscaled)
   float* s_sf = s_thr + C::RWG;                              // [RWG][SF] src features
+  uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_sf + C::RWG * SF);  // [MASKW] this workgroup's mask
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i16 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t rb0 = (int64_t)blockIdx.x * C::RWG;  // first src-list position of the workgroup
@@ -217,6 +219,9 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
     const int64_t si = rb0 + e / SF;
     s_sf[e] = si < a.n_src && a.sfeat ? a.sfeat[rb0 * SF + e] : 0.f;
   }
+  const uint32_t* mw = a.mask ? a.mask + (int64_t)blockIdx.x * a.mask_words : nullptr;
+  const int64_t mlds = mw ? (a.mask_words < C::MASKW ? a.mask_words : C::MASKW) : 0;
+  for (int64_t w = tid; w < mlds; w += 256) s_mask[w] = mw[w];
   __syncthreads();  // no DMA in flight yet: a plain barrier
   const float tmax_sc = a.tmax_norm * a.tsc;
 #pragma unroll
@@ -231,14 +236,15 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
                   : t0 == -INFINITY ? 1.01f * s_sf[wrow * SF + TOPK_M + 2] * a.ssc * tmax_sc + 1.f : -(t0 * a.scaled);
     }
 
-  // the chunk sequence: the set bits of this workgroup's mask (every chunk without one), ascending
-  const uint32_t* mw = a.mask ? a.mask + (int64_t)blockIdx.x * a.mask_words : nullptr;
+  // the chunk sequence: the set bits of this workgroup's mask (every chunk without one), ascending;
+  // the mask words come from LDS (beyond MASKW words: global memory)
   auto next_chunk = [&](int64_t x) -> int64_t {  // smallest chunk > x in the sequence (nch: none)
     int64_t c = x + 1;
     if (!mw) return c < nch ? c : nch;
     while (c < nch) {
       const int64_t w = c >> 5;
-      const uint32_t bits = (uint32_t)__builtin_amdgcn_readfirstlane((int)mw[w]) >> (c & 31);
+      const uint32_t word = w < mlds ? s_mask[w] : mw[w];
+      const uint32_t bits = (uint32_t)__builtin_amdgcn_readfirstlane((int)word) >> (c & 31);
       if (bits) {
         c += __builtin_ctz(bits);
         return c < nch ? c : nch;
@@ -249,7 +255,8 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
   };
 
   // DMA of chunk c into ring slot `slot`: the wave's DPW KiB of rows (source addresses carry the
-  // unit swizzle, the LDS image is lane-linear)
+  // unit swizzle, the LDS image is lane-linear), then the wave's own copy of the chunk's bound box
+  // (48 B, lanes 0-2)
   auto dma = [&](int64_t c, int slot) __attribute__((always_inline)) {
     char* base = ring + slot * C::SLOT;
     const int64_t j0 = c * C::CH;
@@ -261,6 +268,9 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       const char* src = Th + (j0 + row) * RB + 16 * (up ^ tk_sw<KP>(row));
       __builtin_amdgcn_global_load_lds((tk_glb_vp)src, (tk_lds_vp)(base + ins * 1024), 16, 0, 0);
     }
+    const float* cf = a.cfeat ? a.cfeat + c * TOPK_CF : a.S;  // any valid address when unpruned
+    if (lane < TOPK_CF / 4)
+      __builtin_amdgcn_global_load_lds((tk_glb_vp)(cf + 4 * lane), (tk_lds_vp)(base + C::CB + wave * 64), 16, 0, 0);
   };
   int64_t c_iss = -1, n_iss = 0;
   for (int u = 0; u < C::NSTG - 1; ++u) {
@@ -378,9 +388,10 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       }
     }
     // can any row of this wave still take a dst row of chunk c (bound + margin >= its threshold)?
+    const char* base = ring + (int)(it % C::NSTG) * C::SLOT;
     bool need = !a.cfeat;
     if (a.cfeat) {
-      const float* cf = a.cfeat + c * TOPK_CF;
+      const float* cf = reinterpret_cast<const float*>(base + C::CB + wave * 64);
       float cfr[TOPK_CF];
 #pragma unroll
       for (int f = 0; f < TOPK_CF; f += 4) {
@@ -398,7 +409,6 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       }
     }
     if (!__any(need)) continue;
-    const char* base = ring + (int)(it % C::NSTG) * C::SLOT;
     const int64_t j0 = c * C::CH;
     f16x8 df[2][NQ];
     auto rd = [&](int J, f16x8 (&d)[NQ]) __attribute__((always_inline)) {
@@ -484,7 +494,10 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
     // fewer than kt listed: the bound below needs t >= every threshold the scan used, which only a
     // list of kt entries guarantees
     if (cnt < a.kt || !((double)kth > (double)t + e)) {
-      if (lane == 0) a.need_exact[so] = 1;
+      if (lane == 0) {
+        a.need_exact[so] = 1;
+        if (a.kth0) a.kth0[so] = kth;  // a lower bound of the true k-th F2J score: the rescan's start
+      }
     }
   }
   if (lane < k) {
@@ -720,7 +733,10 @@ __global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32
 #pragma unroll
   for (int h = 0; h < 2 * P; ++h) { bs[h] = -INFINITY; bi[h] = -1; }
   int nin = 0;                // newcomer batches buffered (wave-uniform)
-  float thr = -INFINITY;      // the kept list's last score once full
+  // the kept list's last score once full; a rescan starts from the certification pass's k-th exact
+  // score (a lower bound of the true k-th: rows strictly below it cannot enter the top-k)
+  const float thr_init = a.kth0 ? a.kth0[si] : -INFINITY;
+  float thr = thr_init;
   // this row's bound features (fp64, like the order kernel's)
   float sfe[TOPK_M + 1];
   float marg = 0.f;
@@ -766,7 +782,7 @@ __global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32
 #pragma unroll
       for (int h = P; h < 2 * P; ++h) { bs[h] = -INFINITY; bi[h] = -1; }
       nin = 0;
-      thr = rdlane(bs[P - 1], 63);
+      thr = fmaxf(thr_init, rdlane(bs[P - 1], 63));
     }
   }
   wave_bitonic<2 * P>(bs, bi);

@@ -21,6 +21,7 @@ for s in "$@"; do
     bench_c5) timeout -k 10 400 python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err ;;
     prof_c4) timeout -k 10 1100 tools/prof.sh c4 r03 16384 > gpurun_out/prof_c4.log 2>&1 ;;
     trace_c4) mkdir -p gpurun_out/trace_c4 && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_c4 -o run -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu --topk-users 16384 > gpurun_out/trace_c4/bench.json 2> gpurun_out/trace_c4/bench.err ;;
+    trace_topk) mkdir -p gpurun_out/trace_topk && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_topk -o run -- python3 -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/trace_topk/bench.json 2> gpurun_out/trace_topk/bench.err ;;
     tests_mr) timeout -k 10 900 $PYT tests/test_multi_rank.py > gpurun_out/tests_mr.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
