@@ -107,6 +107,7 @@ struct Side {
   int64_t own_nnz = 0;
   std::vector<int64_t> h_deg;    // degree per own row
   DevBuf d_rows;                 // own local rows grouped by bucket
+  DevBuf d_desc;                 // int4 per d_rows entry: {row, p0 lo, p0 hi, degree} (light16 prefetch)
   int64_t boff[NBUCKET + 1] = {0};
   int64_t bnnz[NBUCKET] = {0};
   float vmax = 0.f;              // max |rating| over own dst rows (heavy-build fp16 scaling)
@@ -392,6 +393,9 @@ int rank_layout(als_ctx* c) {
     S.boff[NBUCKET] = (int64_t)all.size();
     HIPCHK(S.d_rows.ensure(all.size() * 4));
     HIPCHK(hipMemcpy(S.d_rows.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(S.d_desc.ensure(all.size() * 16));
+    HIPCHK(launch_row_desc(S.d_rows.as<int32_t>(), (int64_t)all.size(), S.d_ptr.as<int64_t>(), S.d_desc.as<int32_t>(), c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
     // split-K chunks of each solve chunk's heaviest rows (a prefix of its heavy run: by degree);
     // slot0 is chunk-local (starts at 0 for every solve chunk)
     const int64_t CH = c->split_len;
@@ -446,7 +450,8 @@ int factor_buffers(als_ctx* c) {
     Side& S = c->s[side];
     // X padded to whole layout chunks (zero rows past own_n: they travel in the chunk gathers)
     HIPCHK(S.d_X.ensure((size_t)std::max<int64_t>(std::max<int64_t>(S.own_n, (int64_t)S.nch * S.chpad), 1) * c->KP * 4));
-    HIPCHK(S.d_Z.ensure((size_t)std::max<int64_t>(S.prows(), 1) * c->KP * 4));
+    // + one zero row at prows(): the gather target of masked light-row entries (never written)
+    HIPCHK(S.d_Z.ensure((size_t)(S.prows() + 1) * c->KP * 4));
     HIPCHK(hipMemset(S.d_X.p, 0, S.d_X.bytes));
     HIPCHK(hipMemset(S.d_Z.p, 0, S.d_Z.bytes));
     if (c->world > 1) {
@@ -897,6 +902,7 @@ int half_sweep(als_ctx* c, int t) {
   a.reg = (float)c->p.reg_param;
   a.err = c->d_err.as<int>();
   a.colscale = c->d_cs.as<float>();
+  a.n_cu = c->n_cu;
   const int32_t* rows = T.d_rows.as<int32_t>();
   static const int Dof[3] = {16, 32, 64};
   T.stats[0] = T.stats[1] = T.stats[2] = T.stats[3] = 0;
@@ -911,6 +917,7 @@ int half_sweep(als_ctx* c, int t) {
   for (int q = 0; q < T.nsolve; ++q) {
     for (int b = 0; b < 3; ++b) {
       a.rows = rows + T.cb[b][q];
+      a.desc = T.d_desc.as<int32_t>() + 4 * T.cb[b][q];
       a.n_rows = T.cb[b][q + 1] - T.cb[b][q];
       if (force_heavy && use_wave_kernel(c)) HIPCHK(launch_solve_wave(KP, a, st));
       else if (force_heavy) HIPCHK(launch_solve_heavy(KP, a, st));
@@ -1131,6 +1138,7 @@ int als_fork(als_ctx* parent, const als_params* p, als_ctx** out) {
     S.d_col.share(P.d_col);
     S.d_val.share(P.d_val);
     S.d_rows.share(P.d_rows);
+    S.d_desc.share(P.d_desc);
     S.d_chunk_row.share(P.d_chunk_row);
     S.d_chunk_idx.share(P.d_chunk_idx);
     S.d_slot0.share(P.d_slot0);

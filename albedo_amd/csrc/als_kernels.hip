@@ -18,6 +18,7 @@
 // lane issues one float4 (16-B) load: sub-step m of chunk c0 contracts column c0 + 4(l>>4) + m.
 #include <hip/hip_runtime.h>
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <type_traits>
 #include <algorithm>
@@ -267,24 +268,16 @@ hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64
 __host__ __device__ constexpr int light_wave_lds(int D) { return D == 16 ? D * (D + 1) / 2 + 64 : 512 + (D / 16) * 256; }
 
 template <int KP, int D>
-__global__ __launch_bounds__(256, (D == 16 && KP <= 128) ? 6 : (KP <= 128) ? 4 : 2) void solve_light_kernel(SolveArgs a) {
-  constexpr int NB = D / 16, NT = NB * (NB + 1) / 2, TRI = light_wave_lds(D), NHC = KP / 64;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
-  float* Ks = smem + wave * TRI;
-  const int64_t ridx = (int64_t)blockIdx.x * 4 + wave;
-  if (ridx >= a.n_rows) return;  // wave-uniform; this kernel has no workgroup barrier
-  const int j = a.rows[ridx];
-  const int64_t p0 = a.ptr[j];
-  const int d = (int)(a.ptr[j + 1] - p0);
+constexpr int light_occupancy() { return (D == 16 && KP <= 128) ? 6 : (KP <= 128) ? 4 : 2; }
 
-  float r = 0.f, ce = 0.f, we = 0.f;
-  int colE = 0;
-  if (lane < d) {
-    r = a.val[p0 + lane];
-    colE = a.col[p0 + lane];
-    rating_weights(r, a.implicit, a.alpha, ce, we);
-  }
+// One light row: j, degree d (wave-uniform), lane e < d holds rating r and src row colE of entry e.
+template <int KP, int D>
+__device__ __forceinline__ void light_row(const SolveArgs& a, int j, int d, float r, int colE, float* smem, int wave) {
+  constexpr int NB = D / 16, NT = NB * (NB + 1) / 2, TRI = light_wave_lds(D), NHC = KP / 64;
+  const int lane = threadIdx.x & 63, g = lane >> 4, i16 = lane & 15;
+  float* Ks = smem + wave * TRI;
+  float ce = 0.f, we = 0.f;
+  if (lane < d) rating_weights(r, a.implicit, a.alpha, ce, we);
   const bool valid = lane < d && ce > 0.f;
   const int npos = a.implicit ? __popcll(__ballot(lane < d && r > 0.f)) : d;
   const float lamn = a.reg * (float)npos;
@@ -526,18 +519,47 @@ __global__ __launch_bounds__(256, (D == 16 && KP <= 128) ? 6 : (KP <= 128) ? 4 :
   }
 }
 
+// One wave per row; the row's descriptor {row, p0, degree} is one scalar load (a.desc) instead of
+// the dependent rows -> ptr pair.  (A persistent, prefetching variant of this kernel measured slower
+// at c4: its scratch spills and conservative waits serialised the gathers; light16.hip has it.)
+template <int KP, int D>
+__global__ __launch_bounds__(256, (light_occupancy<KP, D>())) void solve_light_kernel(SolveArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t ridx = (int64_t)blockIdx.x * 4 + wave;
+  if (ridx >= a.n_rows) return;  // wave-uniform; this kernel has no workgroup barrier
+  typedef __attribute__((address_space(4))) const int cint;
+  cint* q = (cint*)(a.desc) + 4 * ridx;  // constant address space: s_load_dwordx4
+  const int j = q[0], d = q[3];
+  const int64_t p0 = (int64_t)(uint32_t)q[1] | ((int64_t)q[2] << 32);
+  float r = 0.f;
+  int colE = 0;
+  if (lane < d) {
+    r = a.val[p0 + lane];
+    colE = a.col[p0 + lane];
+  }
+  light_row<KP, D>(a, j, d, r, colE, smem, wave);
+}
+
 hipError_t launch_solve_light(int KP, int D, const SolveArgs& a0, hipStream_t s) {
   if (a0.n_rows <= 0) return hipSuccess;
+  // d <= 16: the instruction-count kernel (light16.hip); ALBEDO_LIGHT16=0 keeps this one (A/B)
+  static const bool l16 = [] { const char* e = std::getenv("ALBEDO_LIGHT16"); return !(e && e[0] == '0'); }();
+  if (D == 16 && l16) return launch_solve_light16(KP, a0, s);
+  if (!a0.desc) return hipErrorInvalidValue;
   if (a0.n_rows > max_rows_per_launch(64)) {  // 64 work-items per row: see max_rows_per_launch
     for (int64_t r0 = 0; r0 < a0.n_rows; r0 += max_rows_per_launch(64)) {
-      const hipError_t e = launch_solve_light(KP, D, chunk_args(a0, r0, 64, 0), s);
+      SolveArgs b = chunk_args(a0, r0, 64, 0);
+      b.desc = a0.desc + 4 * r0;
+      const hipError_t e = launch_solve_light(KP, D, b, s);
       if (e != hipSuccess) return e;
     }
     return hipSuccess;
   }
   const SolveArgs& a = a0;
-  const int blocks = (int)((a.n_rows + 3) / 4);
   const size_t lds = ((size_t)4 * light_wave_lds(D) + (size_t)4 * KP) * sizeof(float);  // per-wave K / scratch + D^-1/2
+  const int blocks = (int)((a.n_rows + 3) / 4);
 #define LIGHT(kp, dd) \
   if (KP == kp && D == dd) { solve_light_kernel<kp, dd><<<blocks, 256, lds, s>>>(a); return hipGetLastError(); }
   LIGHT(64, 16) LIGHT(64, 32) LIGHT(64, 64) LIGHT(128, 16) LIGHT(128, 32) LIGHT(128, 64)

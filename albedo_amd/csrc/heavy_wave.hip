@@ -293,9 +293,30 @@ __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
   const int npos = wave_build<KP, IMPLICIT, PRE>(a, p0, d, st, s_cs, acc, bacc);
   const float lamn = a.reg * (float)(IMPLICIT ? npos : d);
   const float* isc = s_cs + KP;
+  // The system is scaled by s2 = 4^e (exact) so that its largest diagonal entry stays below 2^28:
+  // every Cholesky entry |U_ij| <= sqrt(A_jj) is then below 2^14, the range the split-fp16 trailing
+  // updates of wave_chol_solve<NQ, true> need.  x is unchanged ((s2·A') x = s2·b').
+  float dmax = 0.f;
+  static_for<0, NQ>([&](auto AA) {
+    constexpr int A = decltype(AA)::value, t = tix(A, A, NQ);
+    const int c = 16 * A + i16;
+    const float ic = isc[c];
+    float dv = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dv = (4 * q + r == i16) ? acc[t][r] : dv;
+    const float dadd = c < a.kreal ? a.lam[c] + lamn : 1.0f;
+    dmax = fmaxf(dmax, fabsf(dv * (ic * ic) + dadd));
+  });
+  for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o));
+  int ex = 0;
+  frexpf(dmax, &ex);  // dmax < 2^ex
+  int e2 = (28 - ex) >> 1;
+  e2 = e2 > 60 ? 60 : (e2 < -60 ? -60 : e2);
+  const float s2 = ldexpf(1.f, 2 * e2);
   static_for<0, NQ>([&](auto AA) {
     constexpr int A = decltype(AA)::value;
-    const f32x4 ir = ld4(isc + 16 * A + 4 * q);
+    const f32x4 ir = ld4(isc + 16 * A + 4 * q) * s2;
+    bacc[A] *= s2;
     static_for<A, NQ>([&](auto BB) {
       constexpr int B = decltype(BB)::value, t = tix(A, B, NQ);
       const float ic = isc[16 * B + i16];
@@ -303,7 +324,7 @@ __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
       for (int r = 0; r < 4; ++r) acc[t][r] *= ir[r] * ic;
       if constexpr (A == B) {
         const int c = 16 * A + i16;
-        const float dadd = c < a.kreal ? a.lam[c] + lamn : 1.0f;
+        const float dadd = (c < a.kreal ? a.lam[c] + lamn : 1.0f) * s2;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (4 * q + r == i16) acc[t][r] += dadd;
@@ -317,7 +338,7 @@ __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
 #endif
   // ---- blocked Cholesky A' = UᵀU on the tiles, RHS alongside (wave_chol.h) -----------------------
   float xs[NQ];
-  const bool notpd = wave_chol_solve<NQ>(acc, bacc, reinterpret_cast<float*>(st), xs);
+  const bool notpd = wave_chol_solve<NQ, true>(acc, bacc, reinterpret_cast<float*>(st), xs);
   bool nonfinite = false;
 #pragma unroll
   for (int A = 0; A < NQ; ++A) {

@@ -32,6 +32,8 @@ struct SolveArgs {
   int64_t zero_row;        // an all-zero row of Zhl (the gather target of ratings past a row's end)
   float wsc;               // power-of-two scale of the rating weights w in the b' MFMA (max|w|·wsc < 2^13)
   float inv_sw;            // 1 / √c
+  const int32_t* desc;     // light launches: int4 {row, p0 lo, p0 hi, degree} per entry of `rows` (or null)
+  int n_cu;                // compute units (persistent launches)
 };
 
 // Split-K of the heavy tail (rows with more ratings than one chunk): every chunk of chunk_len
@@ -65,6 +67,10 @@ hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64
 
 // Per-row solves. light: rows with degree <= D (D in {16,32,64}); heavy: any degree.
 hipError_t launch_solve_light(int KP, int D, const SolveArgs& a, hipStream_t s);
+// light rows of degree <= 16 (light16.hip): the push-through solve written for VALU instruction count
+hipError_t launch_solve_light16(int KP, const SolveArgs& a, hipStream_t s);
+// desc[4i .. 4i+3] = {rows[i], ptr[rows[i]] lo, hi, degree}: one scalar load per row for light16
+hipError_t launch_row_desc(const int32_t* rows, int64_t n, const int64_t* ptr, int32_t* desc, hipStream_t s);
 hipError_t launch_solve_heavy(int KP, const SolveArgs& a, hipStream_t s);
 // heavy rows, one wave per row (heavy_wave.hip), KP <= 128; rows of any degree (split rows excepted)
 hipError_t launch_solve_wave(int KP, const SolveArgs& a, hipStream_t s);

@@ -23,7 +23,31 @@ namespace albedo {
 // upper tile (a <= b) index, row-major over the upper triangle
 __host__ __device__ constexpr int tix(int a, int b, int nq) { return a * nq - a * (a - 1) / 2 + (b - a); }
 
-template <int NQ>
+// fp16 hi (slots 0..3) and lo (slots 4..7) of four fp32 values: packed RNE conversion for hi, lo =
+// fp16(x - hi) by v_fma_mix (x·1 - hi is exact in fp32, so one rounding)
+__device__ __forceinline__ f16x8 split_hilo4(f32x4 v) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef float f32x2v __attribute__((ext_vector_type(2)));
+  uint32_t w[4];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const f16x2 h = __builtin_convertvector((f32x2v{v[2 * p], v[2 * p + 1]}), f16x2);
+    w[p] = __builtin_bit_cast(uint32_t, h);
+    uint32_t l;
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%3 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %0, %2, 1.0, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "=&v"(l) : "v"(v[2 * p]), "v"(v[2 * p + 1]), "v"(w[p]));
+    w[2 + p] = l;
+  }
+  return __builtin_bit_cast(f16x8, (u32x4{w[0], w[1], w[2], w[3]}));
+}
+
+// SPLIT: the trailing updates T -= UᵀU run on v_mfma_f32_16x16x32_f16 with U split into fp16 hi + lo
+// (hi·hi + hi·lo + lo·hi in two MFMAs: k-slots 0..3 / 4..7 of a lane carry the same four rows as hi /
+// lo, so the operands come straight from the C/D registers) instead of four f32 MFMAs: 32 instead of
+// 128 matrix-core cycles per tile update.  The caller scales the system so that every U entry is
+// below 2^14 (|U_ij| <= sqrt(A_jj): max diagonal < 2^28), keeping hi and lo in fp16's normal range.
+template <int NQ, bool SPLIT = false>
 __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2], float (&bacc)[NQ], float* scr,
                                                 float (&xs)[NQ]) {
   const int lane = threadIdx.x & 63, q = lane >> 4, i16 = lane & 15;
@@ -98,14 +122,34 @@ __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2],
       bacc[M] -= pv;
     });
     // trailing tiles: T(M, I) -= U(jb, M)ᵀ U(jb, I), the next diagonal tile first
-    static_for<jb + 1, NQ>([&](auto MM) {
-      constexpr int M = decltype(MM)::value, tm = tix(jb, M, NQ);
-      static_for<M, NQ>([&](auto II) {
-        constexpr int I = decltype(II)::value, t = tix(M, I, NQ), ti = tix(jb, I, NQ);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc[t] = mfma4(-acc[tm][s], acc[ti][s], acc[t]);
+    if constexpr (SPLIT) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      f16x8 ub[NQ];  // B operands [hi | lo] of the panel row's tiles
+      static_for<jb + 1, NQ>([&](auto II) {
+        constexpr int I = decltype(II)::value;
+        ub[I] = split_hilo4(acc[tix(jb, I, NQ)]);
       });
-    });
+      static_for<jb + 1, NQ>([&](auto MM) {
+        constexpr int M = decltype(MM)::value;
+        const u32x4 w = __builtin_bit_cast(u32x4, ub[M]) ^ 0x80008000u;  // -hi, -lo
+        const f16x8 a1 = __builtin_bit_cast(f16x8, (u32x4{w[0], w[1], w[0], w[1]}));  // [-hi | -hi]
+        const f16x8 a2 = __builtin_bit_cast(f16x8, (u32x4{w[2], w[3], 0u, 0u}));      // [-lo | 0]
+        static_for<M, NQ>([&](auto II) {
+          constexpr int I = decltype(II)::value, t = tix(M, I, NQ);
+          acc[t] = mfma_h(a1, ub[I], acc[t]);  // -(hi_M·hi_I + hi_M·lo_I)
+          acc[t] = mfma_h(a2, ub[I], acc[t]);  // -(lo_M·hi_I)
+        });
+      });
+    } else {
+      static_for<jb + 1, NQ>([&](auto MM) {
+        constexpr int M = decltype(MM)::value, tm = tix(jb, M, NQ);
+        static_for<M, NQ>([&](auto II) {
+          constexpr int I = decltype(II)::value, t = tix(M, I, NQ), ti = tix(jb, I, NQ);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc[t] = mfma4(-acc[tm][s], acc[ti][s], acc[t]);
+        });
+      });
+    }
     WAVE_LDS_SYNC();  // scratch reads done before the next panel rewrites it
   });
 
