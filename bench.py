@@ -165,8 +165,8 @@ def main():
     # tools/traffic.py; rocprof cannot run inside the timed bench): GB per sweep, like bytes_per_sweep
     # The heavy timer covers every kernel of the explicit path: split-K partials + reduce, the wave
     # kernel, the workgroup kernel (and, with nonnegative, the NNLS kernels)
-    timer_kernels = {"solve_light": ("solve_light",),
-                     "solve_heavy": ("solve_wave", "solve_heavy", "heavy_partial", "heavy_reduce"),
+    timer_kernels = {"solve_light": ("solve_light", "solve_light16"),
+                     "solve_heavy": ("solve_wave", "solve_heavy", "wave_partial", "heavy_partial", "heavy_reduce"),
                      "nnls_batch": ("nnls_batch",),
                      "solve_nnls": ("solve_nnls", "heavy_partial", "heavy_reduce")}[dom]
     traffic = None

@@ -20,10 +20,15 @@ for s in "$@"; do
     bench_c2) timeout -k 10 300 python -u bench.py --config c2 --steps 10 --warmup 5 > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.err ;;
     bench_c5) timeout -k 10 400 python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err ;;
     prof_c4) timeout -k 10 1100 tools/prof.sh c4 r03 16384 > gpurun_out/prof_c4.log 2>&1 ;;
+    prof_c5) timeout -k 10 900 tools/prof.sh c5 r03 0 > gpurun_out/prof_c5.log 2>&1 ;;
+    prof_c2) timeout -k 10 600 tools/prof.sh c2 r03 16384 > gpurun_out/prof_c2.log 2>&1 ;;
     trace_c4) mkdir -p gpurun_out/trace_c4 && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_c4 -o run -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu --topk-users 16384 > gpurun_out/trace_c4/bench.json 2> gpurun_out/trace_c4/bench.err ;;
     trace_topk) mkdir -p gpurun_out/trace_topk && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_topk -o run -- python3 -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/trace_topk/bench.json 2> gpurun_out/trace_topk/bench.err ;;
     ab_c4) for v in 0 1; do ALBEDO_LIGHT16=$v timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu --topk-users 0 > gpurun_out/ab_c4_$v.json 2> gpurun_out/ab_c4_$v.err || exit 1; done ;;
     tests_solve) timeout -k 10 700 $PYT tests/test_gpu_parity.py tests/test_gpu_heavy_tail.py tests/test_gpu_scale.py -k "half_sweep or golden or facade or albedo_protocol or column_scaling or positive_definite or heavy or c4_scale_rows or c2_scale" > gpurun_out/tests_solve.log 2>&1 ;;
+    tests_nnls) timeout -k 10 700 $PYT tests/test_gpu_parity.py tests/test_gpu_heavy_tail.py tests/test_gpu_c5_rows.py -k "nnls or c5" > gpurun_out/tests_nnls.log 2>&1 ;;
+    ab_c5) for v in 0 1; do ALBEDO_NNLS_REG=$v timeout -k 10 400 python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/ab_c5_$v.json 2> gpurun_out/ab_c5_$v.err || exit 1; done ;;
+    probe_bo) ALBEDO_ALS_LIB=tools/probe/libwave_buildonly.so timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/probe_bo.json 2> gpurun_out/probe_bo.err || true ;;
     tests_mr) timeout -k 10 900 $PYT tests/test_multi_rank.py > gpurun_out/tests_mr.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -12,6 +12,7 @@ import collections
 import csv
 import glob
 import json
+import re
 import sys
 
 
@@ -24,7 +25,8 @@ def per_kernel(path, counter):
                 continue
             k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
             k = k.replace("void ", "").replace("albedo::", "")
-            base = k.split("<")[0].replace("_kernel", "")
+            m = re.search(r"([a-z][a-z0-9_]*)_kernel", k)  # also mangled names (anonymous-namespace kernels)
+            base = m.group(1) if m else k.split("<")[0]
             tot[base] += float(r["Counter_Value"])
             nd[base].add(r["Dispatch_Id"])
     return tot, {k: len(v) for k, v in nd.items()}
@@ -38,7 +40,7 @@ def main():
                       "--steps 1 --warmup 0 --no-cpu --topk-users 0`; FETCH_SIZE x2 (gfx950 wide-read correction); "
                       "GB (1e9 B) per sweep, summed over the kernel's launches"}
     for k in sorted(set(fetch) | set(write)):
-        if not k.startswith(("solve_", "gram", "rotate", "topk", "heavy_")):
+        if not k.startswith(("solve_", "gram", "rotate", "topk", "heavy_", "wave_", "presplit", "colmax", "nnls_")):
             continue
         f_gb = 2.0 * fetch.get(k, 0.0) * 1024 / 1e9
         w_gb = write.get(k, 0.0) * 1024 / 1e9
