@@ -290,7 +290,7 @@ __device__ __forceinline__ void light_row(const SolveArgs& a, int j, int d, floa
     vB[I] = __shfl((int)valid, 16 * I + i16) != 0;
   }
   constexpr int NC = KP / 16;
-  constexpr bool KEEPZ = D <= 32 && D * KP <= 4096;  // keep the gathered rows in registers for x'
+  constexpr bool KEEPZ = D <= 32 && D * KP <= 4096;  // keep the gathered rows in registers for x' (D = 64 at KP = 128, 2 waves per SIMD: measured slower)
   f32x4 zf[KEEPZ ? NB : 1][KEEPZ ? NC : 1];
   if constexpr (KEEPZ) {  // issue every gather up front: one latency for the whole row
 #pragma unroll
