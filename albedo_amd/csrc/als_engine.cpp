@@ -607,10 +607,11 @@ float event_ms(hipEvent_t a, hipEvent_t b) {
 }
 
 // fp16 column scales of the heavy build for dst side T over the gathered src rows Z
-int column_scales(als_ctx* c, const Side& S, const Side& T) {
+// have_max: the rotation left the column maxima of Z in d_csmax (rotate_kernel's epilogue)
+int column_scales(als_ctx* c, const Side& S, const Side& T, bool have_max = false) {
   const float cmax = c->p.implicit_prefs ? (float)c->p.alpha * T.vmax : 1.0f;
   HIPCHK(launch_colscale(c->KP, S.d_Z.as<float>(), S.prows(), cmax, c->d_csmax.as<unsigned>(),
-                         c->d_cs.as<float>(), c->st));
+                         c->d_cs.as<float>(), c->st, have_max));
   return ALS_OK;
 }
 
@@ -805,6 +806,7 @@ int half_sweep(als_ctx* c, int t) {
   hipEvent_t* ev = c->ev;
   const bool multi = c->world > 1;
   double eig_ms = 0.0;
+  bool have_cmax = false;
   bool force_heavy = c->p.light_max_degree == 0;
   // world > 1: the previous half's factor gathers (second stream) finish before any collective or
   // rotation of this one is issued -- two RCCL operations of one communicator must never overlap
@@ -866,9 +868,13 @@ int half_sweep(als_ctx* c, int t) {
     HIPCHK(hipMemcpyAsync(c->d_P.p, P32.data(), P32.size() * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(c->d_lam.p, lam32.data(), lam32.size() * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(ev[2], st));
-    // world > 1: every rank rotates the whole gathered src (no collective on the critical path)
-    if (multi) HIPCHK(launch_rotate(KP, S.d_Xfull.as<float>(), c->d_P.as<float>(), S.d_Z.as<float>(), S.prows(), st));
-    else HIPCHK(launch_rotate(KP, S.d_X.as<float>(), c->d_P.as<float>(), S.d_Z.as<float>(), S.own_n, st));
+    // world > 1: every rank rotates the whole gathered src (no collective on the critical path);
+    // the rotation also leaves the column maxima of Z for the heavy build's column scales
+    HIPCHK(hipMemsetAsync(c->d_csmax.p, 0, KP * sizeof(unsigned), st));
+    unsigned* cm = c->d_csmax.as<unsigned>();
+    if (multi) HIPCHK(launch_rotate(KP, S.d_Xfull.as<float>(), c->d_P.as<float>(), S.d_Z.as<float>(), S.prows(), st, cm));
+    else HIPCHK(launch_rotate(KP, S.d_X.as<float>(), c->d_P.as<float>(), S.d_Z.as<float>(), S.own_n, st, cm));
+    have_cmax = true;
   } else {
     HIPCHK(hipEventRecord(ev[1], st));
     HIPCHK(hipMemsetAsync(c->d_lam.p, 0, KP * 4, st));
@@ -879,7 +885,7 @@ int half_sweep(als_ctx* c, int t) {
     else HIPCHK(hipMemcpyAsync(S.d_Z.p, S.d_X.p, (size_t)S.own_n * KP * 4, hipMemcpyDeviceToDevice, st));
   }
   HIPCHK(hipEventRecord(ev[3], st));
-  TRYC(column_scales(c, S, T));
+  TRYC(column_scales(c, S, T, have_cmax));
   const void* zhl = nullptr;
   float wsc = 1.f, inv_sw = 1.f;
   TRYC(presplit(c, S, T, &zhl, &wsc, &inv_sw));

@@ -188,14 +188,20 @@ template <int KP> constexpr int rotate_cols() { return KP >= 256 ? 128 : KP; }  
 // 8 waves per block share one LDS copy of M (64+ KB); each wave's
 // 16 rows are loaded whole before the first MFMA.
 constexpr int ROT_WAVES = 8;
+// cmax (or null): bits of max_rows |Z[.][c]| accumulated with atomicMax (zeroed by the caller) -- the
+// column maxima the heavy build's fp16 column scales need, without a second pass over Z
 template <int KP>
 __global__ __launch_bounds__(64 * ROT_WAVES) void rotate_kernel(const float* __restrict__ X,
                                                                const float* __restrict__ M,
-                                                               float* __restrict__ Z, int64_t n) {
+                                                               float* __restrict__ Z, int64_t n,
+                                                               unsigned* __restrict__ cmax) {
   constexpr int NO = rotate_cols<KP>(), LDM = NO + 4, NJ = NO / 16, NC = KP / 16;
   constexpr int NTH = 64 * ROT_WAVES, RPB = 16 * ROT_WAVES;  // rows per block iteration
   extern __shared__ __attribute__((aligned(16))) float sM[];
   const int co = blockIdx.y * NO;  // this block's output columns co .. co+NO-1
+  float cm[NJ];
+#pragma unroll
+  for (int J = 0; J < NJ; ++J) cm[J] = 0.f;
   for (int e = threadIdx.x; e < KP * NO / 4; e += NTH) {
     const int r = (4 * e) / NO, c = (4 * e) % NO;
     *reinterpret_cast<f32x4*>(sM + r * LDM + c) = ld4(M + r * KP + co + c);
@@ -231,28 +237,46 @@ __global__ __launch_bounds__(64 * ROT_WAVES) void rotate_kernel(const float* __r
       for (int r = 0; r < 4; ++r) {
         const int64_t rr = b * RPB + wave * 16 + 4 * g + r;
         if (rr < n) Z[rr * KP + co + 16 * J + i16] = acc[J][r];
+        cm[J] = fmaxf(cm[J], fabsf(acc[J][r]));  // rows past n are zero (zero loads)
       }
+  }
+  if (cmax) {  // column maxima: the wave's four lane groups, the block's waves (LDS), one atomic each
+    __syncthreads();  // M's LDS image is dead
+    float* red = sM;  // [ROT_WAVES][NO]
+#pragma unroll
+    for (int J = 0; J < NJ; ++J) {
+      float v = cm[J];
+      v = fmaxf(v, __shfl_xor(v, 16));
+      v = fmaxf(v, __shfl_xor(v, 32));
+      if (g == 0) red[wave * NO + 16 * J + i16] = v;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < NO; c += NTH) {
+      float v = red[c];
+      for (int w = 1; w < ROT_WAVES; ++w) v = fmaxf(v, red[w * NO + c]);
+      atomicMax(cmax + co + c, __float_as_uint(v));
+    }
   }
 }
 
-hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64_t n, hipStream_t s) {
+hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64_t n, hipStream_t s, unsigned* cmax) {
   if (n <= 0) return hipSuccess;
   int64_t blocks = (n + 16 * ROT_WAVES - 1) / (16 * ROT_WAVES);
   if (blocks > 1024) blocks = 1024;
   const int nth = 64 * ROT_WAVES;
   if (KP == 64) {
     const size_t lds = (size_t)64 * 68 * 4;
-    rotate_kernel<64><<<(int)blocks, nth, lds, s>>>(X, M, Z, n);
+    rotate_kernel<64><<<(int)blocks, nth, lds, s>>>(X, M, Z, n, cmax);
   } else if (KP == 128) {
     const size_t lds = (size_t)128 * 132 * 4;
     static const hipError_t attr = allow_lds(rotate_kernel<128>, lds);
     if (attr != hipSuccess) return attr;
-    rotate_kernel<128><<<(int)blocks, nth, lds, s>>>(X, M, Z, n);
+    rotate_kernel<128><<<(int)blocks, nth, lds, s>>>(X, M, Z, n, cmax);
   } else if (KP == 256) {
     const size_t lds = (size_t)256 * (rotate_cols<256>() + 4) * 4;
     static const hipError_t attr = allow_lds(rotate_kernel<256>, lds);
     if (attr != hipSuccess) return attr;
-    rotate_kernel<256><<<dim3((int)blocks, 256 / rotate_cols<256>()), nth, lds, s>>>(X, M, Z, n);
+    rotate_kernel<256><<<dim3((int)blocks, 256 / rotate_cols<256>()), nth, lds, s>>>(X, M, Z, n, cmax);
   } else return hipErrorInvalidValue;
   return hipGetLastError();
 }
@@ -1515,7 +1539,11 @@ __global__ void absmax_kernel(const float* __restrict__ v, int64_t n, unsigned* 
 }
 
 hipError_t launch_colscale(int KP, const float* Z, int64_t n, float cmax, unsigned* tmp, float* colscale,
-                           hipStream_t s) {
+                           hipStream_t s, bool have_max) {
+  if (have_max) {  // tmp already holds the column maxima (rotate_kernel)
+    colscale_kernel<<<1, KP, 0, s>>>(tmp, KP, sqrtf(cmax > 0.f ? cmax : 1.f), colscale);
+    return hipGetLastError();
+  }
   hipError_t e = hipMemsetAsync(tmp, 0, KP * sizeof(unsigned), s);
   if (e != hipSuccess) return e;
   if (n > 0) {

@@ -62,6 +62,16 @@ __device__ __forceinline__ float sum16_last(float x) {
   return x;
 }
 
+// Sum over the four 16-lane rows of the wave (lanes l, l^16, l^32, l^48), every lane getting the same
+// value: v_permlane16_swap pairs rows (0,1) and (2,3), v_permlane32_swap the two halves -- VALU only,
+// no LDS round trip (a __shfl_xor is one).  Partners add in the same order: bit-identical results.
+__device__ __forceinline__ float rows4_sum(float x) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  const float s = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 // v_rsq_f32 / v_rcp_f32 / v_sqrt_f32: single instructions (~1 ulp) instead of the IEEE-exact
 // multi-instruction expansions; the solve tolerance is 1e-4 relative (tests state it)
 __device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }

@@ -62,8 +62,10 @@ hipError_t launch_gram(int KP, const float* X, int64_t n, double* slab, int slab
 int gram_slab_blocks(int KP, int64_t n);
 size_t gram_slab_doubles(int KP, int slab_blocks);
 
-// Z = X · M for n rows ([n][KP] · [KP][KP], row-major M).
-hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64_t n, hipStream_t s);
+// Z = X · M for n rows ([n][KP] · [KP][KP], row-major M); cmax (optional, zeroed by the caller):
+// atomicMax of the bits of max |Z[.][c]| per column (launch_colscale(..., have_max = true) reads it)
+hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64_t n, hipStream_t s,
+                         unsigned* cmax = nullptr);
 
 // Per-row solves. light: rows with degree <= D (D in {16,32,64}); heavy: any degree.
 hipError_t launch_solve_light(int KP, int D, const SolveArgs& a, hipStream_t s);
@@ -89,7 +91,7 @@ hipError_t launch_nnls_batch(int KP, int slots, const SolveArgs& a, const void* 
                              unsigned int* counter, int n_cu, hipStream_t s);
 // colscale[c] = 2^e_c with max_rows |Z[.][c]|·√cmax < 2^13, colscale[KP+c] = 2^-e_c (tmp: KP uints)
 hipError_t launch_colscale(int KP, const float* Z, int64_t n, float cmax, unsigned* tmp, float* colscale,
-                           hipStream_t s);
+                           hipStream_t s, bool have_max = false);
 // Zhl[r] = fp16 hi and lo of Z[r][c]·(sw·colscale[c]) (the heavy build's operand split, done once per
 // src row instead of once per gathered rating); row n (the zero row) is cleared
 hipError_t launch_presplit(int KP, const float* Z, int64_t n, const float* colscale, float sw, void* Zhl, hipStream_t s);

@@ -60,6 +60,7 @@ __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2],
     // diagonal tile to the row layout of chol16 (lane i: row i, replicated over the 4 lane groups)
 #pragma unroll
     for (int r = 0; r < 4; ++r) scr[(4 * q + r) * 16 + i16] = acc[td][r];
+    if (q == 0) scr[256 + i16] = bacc[jb];  // b_jb alongside (the L⁻¹ image overwrites it later)
     WAVE_LDS_SYNC();
     float rr[16];
 #pragma unroll
@@ -68,6 +69,7 @@ __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2],
 #pragma unroll
       for (int e = 0; e < 4; ++e) rr[4 * u + e] = v[e];
     }
+    const f32x4 bt = ld4(scr + 256 + 4 * q);  // lane i + 16q: b_jb[4q .. 4q+3] (the MFMA k layout)
     float dg = 1.f;
     notpd |= chol16(rr, dg, i16);
     // chol16 ends in inline asm: two wait states before any DPP read of its results
@@ -75,17 +77,21 @@ __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2],
                  : "+v"(rr[0]), "+v"(rr[1]), "+v"(rr[2]), "+v"(rr[3]), "+v"(rr[4]), "+v"(rr[5]), "+v"(rr[6]),
                    "+v"(rr[7]), "+v"(rr[8]), "+v"(rr[9]), "+v"(rr[10]), "+v"(rr[11]), "+v"(rr[12]),
                    "+v"(rr[13]), "+v"(rr[14]), "+v"(rr[15]), "+v"(dg));
-    // column i16 of L⁻¹: L x = e_i16 by forward substitution, L[r][m] broadcast from lane r
-    float x[16];
-    static_for<0, 16>([&](auto RR) {
-      constexpr int r = decltype(RR)::value;
-      float tv = (i16 == r) ? 1.f : 0.f;
+    // column i16 of L⁻¹: L x = e_i16 by forward substitution, L[r][m] broadcast from lane r.  Right-
+    // looking (x_m, then every later row's update by x_m): the updates of one step are independent, so
+    // the dependent chain is 16 steps long instead of 120 FMAs; each row still accumulates its terms
+    // in increasing m (the same roundings as the dot-product order).
+    float x[16];  // row r's running value until step r, then L⁻¹[r][i16]
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x[r] = (i16 == r) ? 1.f : 0.f;
+    static_for<0, 16>([&](auto MM) {
+      constexpr int m = decltype(MM)::value;
+      x[m] *= bc16_after_asm<m>(dg);
       // one v_fmac_f32_dpp per term (asm keeps the broadcasts from being hoisted into registers)
-      static_for<0, r>([&](auto MM) {
-        constexpr int m = decltype(MM)::value;
-        fnmac_bc16<r, false>(tv, rr[m], x[m]);
+      static_for<m + 1, 16>([&](auto RR) {
+        constexpr int r = decltype(RR)::value;
+        fnmac_bc16<r, false>(x[r], rr[m], x[m]);
       });
-      x[r] = tv * bc16_after_asm<r>(dg);
     });
     if (q == 0) {
 #pragma unroll
@@ -102,24 +108,24 @@ __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2],
       for (int s = 0; s < 4; ++s) u = mfma4(lv[s], acc[t][s], u);
       acc[t] = u;
     });
-    // RHS: y_jb = L⁻¹ b_jb, then b_M -= U(jb, M)ᵀ y_jb for the blocks below
+    // RHS: y_jb = L⁻¹ b_jb, then b_M -= U(jb, M)ᵀ y_jb for the blocks below (VALU + shuffles: the
+    // same products on the f32 MFMA -- 8 + 4 per block -- measured slower, they compete with the
+    // other wave's build for the matrix core)
     float yp = 0.f;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) yp = fmaf(lv[s], __shfl(bacc[jb], 4 * q + s), yp);
-    yp += __shfl_xor(yp, 16);
-    yp += __shfl_xor(yp, 32);
+    for (int s = 0; s < 4; ++s) yp = fmaf(lv[s], bt[s], yp);
+    yp = rows4_sum(yp);
     bacc[jb] = yp;
-    float y4[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) y4[r] = __shfl(yp, 4 * q + r);
+    // y[4q .. 4q+3] to lane group q through the scratch (the L⁻¹ image's first row is already read)
+    if (q == 0) scr[256 + i16] = yp;
+    WAVE_LDS_SYNC();
+    const f32x4 y4 = ld4(scr + 256 + 4 * q);
     static_for<jb + 1, NQ>([&](auto MM) {
       constexpr int M = decltype(MM)::value, t = tix(jb, M, NQ);
       float pv = 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) pv = fmaf(acc[t][r], y4[r], pv);
-      pv += __shfl_xor(pv, 16);
-      pv += __shfl_xor(pv, 32);
-      bacc[M] -= pv;
+      bacc[M] -= rows4_sum(pv);
     });
     // trailing tiles: T(M, I) -= U(jb, M)ᵀ U(jb, I), the next diagonal tile first
     if constexpr (SPLIT) {
@@ -165,26 +171,19 @@ __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2],
     float tq[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) tq[r] = sum16_last(pr[r]);  // row 4g + r in lane 15 + 16g
-    // lane i + 16q gets t_i = y_i - (row i's sum): row i lives in lane 15 + 16(i >> 2), slot i & 3
-    float ti = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float v = __shfl(tq[r], 15 + 16 * (i16 >> 2));
-      ti = (i16 & 3) == r ? v : ti;
-    }
-    ti = bacc[jb] - ti;
-    // x = L⁻ᵀ t: lane k + 16q holds L⁻¹[k][4q + s]; x[4q + s] = Σ_k L⁻¹[k][4q + s] t_k
+    // lane i + 16q gets t_i = y_i - (row i's sum): row i lives in lane 15 + 16(i >> 2), slot i & 3,
+    // gathered through the scratch (one store + one load instead of four shuffles)
     const f32x4 lv = s_linv[jb * 64 + lane];
+    if (i16 == 15) *reinterpret_cast<f32x4*>(scr + 4 * q) = f32x4{tq[0], tq[1], tq[2], tq[3]};
+    WAVE_LDS_SYNC();
+    const float ti = bacc[jb] - scr[i16];
+    // x = L⁻ᵀ t: lane k + 16q holds L⁻¹[k][4q + s]; x[4q + s] = Σ_k L⁻¹[k][4q + s] t_k
     float xq[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) xq[s] = sum16_last(lv[s] * ti);  // x[4g + s] in lane 15 + 16g
-    float xi = 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const float v = __shfl(xq[s], 15 + 16 * (i16 >> 2));
-      xi = (i16 & 3) == s ? v : xi;
-    }
-    xs[jb] = xi;
+    if (i16 == 15) *reinterpret_cast<f32x4*>(scr + 16 + 4 * q) = f32x4{xq[0], xq[1], xq[2], xq[3]};
+    WAVE_LDS_SYNC();
+    xs[jb] = scr[16 + i16];
   });
   return notpd;
 }
