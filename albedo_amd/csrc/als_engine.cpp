@@ -139,6 +139,7 @@ struct Side {
   // chunk lists start at ck_off[q] and their (chunk-local) slot0 at sl_off[q]
   int nsolve = 1;
   int64_t cb[NBUCKET][9] = {{0}};
+  int64_t c8[8] = {0};           // bucket B_L16, solve chunk q: its first c8[q] rows have degree <= 8 (paired)
   int64_t split_n[8] = {0}, ck_off[9] = {0}, sl_off[8] = {0};
 };
 
@@ -331,6 +332,13 @@ int gather_chunk_count() {
   return std::max(1, std::min(8, n));
 }
 
+// Light rows of degree <= 16 take light16.hip (pairs of degree <= 8 rows, then singles) unless
+// ALBEDO_LIGHT16=0 (the generic solve_light_kernel<KP, 16>: A/B)
+bool light16_on() {
+  static const bool on = [] { const char* e = std::getenv("ALBEDO_LIGHT16"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 // Heavy rows at padded rank <= 128 run one wave per row (heavy_wave.hip) unless ALBEDO_HEAVY=wg
 // selects the 4-wave workgroup kernel (A/B measurements); rank 256 always uses the workgroup kernel.
 bool use_wave_kernel(const als_ctx* c);
@@ -381,13 +389,24 @@ int rank_layout(als_ctx* c) {
     all.reserve(S.own_n);
     for (int b = 0; b < NBUCKET; ++b) {
       S.boff[b] = (int64_t)all.size();
-      if (nsolve > 1)
-        std::stable_sort(rows[b].begin(), rows[b].end(), [&](int32_t x, int32_t y) { return chunk_of(x) < chunk_of(y); });
+      // grouped by solve chunk; B_L16: within a chunk the rows of degree <= 8 first (light16 pairs them)
+      const bool pairs = b == B_L16;
+      std::stable_sort(rows[b].begin(), rows[b].end(), [&](int32_t x, int32_t y) {
+        const int cx = chunk_of(x), cy = chunk_of(y);
+        if (cx != cy || !pairs) return cx < cy;
+        return (S.h_deg[x] <= 8) > (S.h_deg[y] <= 8);
+      });
       int64_t p = 0;
       for (int q = 0; q <= nsolve; ++q) {
         while (q < nsolve && p < (int64_t)rows[b].size() && chunk_of(rows[b][p]) < q) ++p;
         S.cb[b][q] = S.boff[b] + (q == nsolve ? (int64_t)rows[b].size() : p);
       }
+      if (pairs)
+        for (int q = 0; q < nsolve; ++q) {
+          int64_t k = 0;
+          for (int64_t i = S.cb[b][q] - S.boff[b]; i < S.cb[b][q + 1] - S.boff[b] && S.h_deg[rows[b][i]] <= 8; ++i) ++k;
+          S.c8[q] = k;
+        }
       all.insert(all.end(), rows[b].begin(), rows[b].end());
     }
     S.boff[NBUCKET] = (int64_t)all.size();
@@ -927,7 +946,15 @@ int half_sweep(als_ctx* c, int t) {
       a.n_rows = T.cb[b][q + 1] - T.cb[b][q];
       if (force_heavy && use_wave_kernel(c)) HIPCHK(launch_solve_wave(KP, a, st));
       else if (force_heavy) HIPCHK(launch_solve_heavy(KP, a, st));
-      else HIPCHK(launch_solve_light(KP, Dof[b], a, st));
+      else if (b == B_L16 && light16_on()) {  // degree <= 8: two rows per wave unit, then the rest
+        SolveArgs p8 = a, p16 = a;
+        p8.n_rows = T.c8[q];
+        p16.rows += T.c8[q];
+        p16.desc += 4 * T.c8[q];
+        p16.n_rows -= T.c8[q];
+        HIPCHK(launch_solve_light16(KP, p8, st, true));
+        HIPCHK(launch_solve_light16(KP, p16, st, false));
+      } else HIPCHK(launch_solve_light(KP, Dof[b], a, st));
     }
     if (T.nsolve == 1) HIPCHK(hipEventRecord(ev[5], st));
     TRYC(heavy_launches(c, T, a, T.cb[B_HEAVY][q], T.cb[B_HEAVY][q + 1] - T.cb[B_HEAVY][q], false, q));
@@ -1157,6 +1184,7 @@ int als_fork(als_ctx* parent, const als_params* p, als_ctx** out) {
     std::memcpy(S.bat_off, P.bat_off, sizeof S.bat_off);
     S.nsolve = P.nsolve;
     std::memcpy(S.cb, P.cb, sizeof S.cb);
+    std::memcpy(S.c8, P.c8, sizeof S.c8);
     std::memcpy(S.split_n, P.split_n, sizeof S.split_n);
     std::memcpy(S.ck_off, P.ck_off, sizeof S.ck_off);
     std::memcpy(S.sl_off, P.sl_off, sizeof S.sl_off);

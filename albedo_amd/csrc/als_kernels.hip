@@ -568,9 +568,6 @@ __global__ __launch_bounds__(256, (light_occupancy<KP, D>())) void solve_light_k
 
 hipError_t launch_solve_light(int KP, int D, const SolveArgs& a0, hipStream_t s) {
   if (a0.n_rows <= 0) return hipSuccess;
-  // d <= 16: the instruction-count kernel (light16.hip); ALBEDO_LIGHT16=0 keeps this one (A/B)
-  static const bool l16 = [] { const char* e = std::getenv("ALBEDO_LIGHT16"); return !(e && e[0] == '0'); }();
-  if (D == 16 && l16) return launch_solve_light16(KP, a0, s);
   if (!a0.desc) return hipErrorInvalidValue;
   if (a0.n_rows > max_rows_per_launch(64)) {  // 64 work-items per row: see max_rows_per_launch
     for (int64_t r0 = 0; r0 < a0.n_rows; r0 += max_rows_per_launch(64)) {

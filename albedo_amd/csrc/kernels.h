@@ -70,7 +70,7 @@ hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64
 // Per-row solves. light: rows with degree <= D (D in {16,32,64}); heavy: any degree.
 hipError_t launch_solve_light(int KP, int D, const SolveArgs& a, hipStream_t s);
 // light rows of degree <= 16 (light16.hip): the push-through solve written for VALU instruction count
-hipError_t launch_solve_light16(int KP, const SolveArgs& a, hipStream_t s);
+hipError_t launch_solve_light16(int KP, const SolveArgs& a, hipStream_t s, bool pair = false);
 // desc[4i .. 4i+3] = {rows[i], ptr[rows[i]] lo, hi, degree}: one scalar load per row for light16
 hipError_t launch_row_desc(const int32_t* rows, int64_t n, const int64_t* ptr, int32_t* desc, hipStream_t s);
 hipError_t launch_solve_heavy(int KP, const SolveArgs& a, hipStream_t s);

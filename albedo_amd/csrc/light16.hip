@@ -33,7 +33,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int L16_LDK = 20;       // row stride of the K / L transposition scratch (floats)
 constexpr int L16_COLS = 64;      // x' columns per LDS stage pass
 constexpr int L16_SLD = L16_COLS + 4;  // stage row stride (floats)
-__host__ __device__ constexpr int l16_wave_floats(int KP) { return 16 * L16_SLD + KP + 16; }
+__host__ __device__ constexpr int l16_wave_floats(int KP) { return 16 * L16_SLD + 2 * KP + 16; }  // stage, D^-1/2 of A, v, of B
 
 // fp16 hi + lo of 8 fp32 values (already rounded to fp32: the caller pins them).  hi: packed RNE
 // conversion; lo = fp16(x - hi) by v_fma_mix{lo,hi}_f16 (x·1 - hi is exact in fp32, so its single
@@ -79,39 +79,60 @@ __device__ __forceinline__ bool entry_valid(const SolveArgs& a, float r, int i16
   return i16 < d && ce > 0.f;
 }
 
-// One row: j, its degree d (wave-uniform), entry i16's rating r and src row colE (every lane group),
-// and the gathered rows zf (lane (i16, g): Z[entry i16][16c + 4g .. +3], zero for masked entries).
-template <int KP>
-__device__ __forceinline__ void light16_row(const SolveArgs& a, int j, int d, float r, int colE,
-                                            const f32x4 (&zf)[KP / 16], float* st, float* sdl, float* vsh,
-                                            const float* s_lam, const float* s_csi, f32x2 (&xo)[KP / 64]) {
+// One unit: a row of degree dA <= 16 (PAIR = false), or two rows of degree <= 8 solved side by side
+// (PAIR: entries 0..7 of the 16-entry tile are row A's, 8..15 row B's; dB = 0 when B is absent).
+// Each lane group holds entry i16's rating r and src row colE and the gathered rows zf (lane (i16, g):
+// Z[entry i16][16c + 4g .. +3], zero for masked entries).  The two rows of a pair share the S tile,
+// the Cholesky steps and the x' stage: K is block diagonal (the cross block is zeroed), so the
+// factorisation of one block never touches the other (L's cross entries stay exactly 0), and each
+// row's arithmetic is the one it would get alone.
+template <int KP, bool PAIR>
+__device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB, float r, int colE,
+                                             const f32x4 (&zf)[KP / 16], float* st, float* sdlA, float* sdlB,
+                                             float* vsh, const float* s_lam, const float* s_csi,
+                                             f32x2 (&xo)[KP / 64]) {
   constexpr int NQ = KP / 32, NHC = KP / 64;
   const int lane = threadIdx.x & 63, g = lane >> 4, i16 = lane & 15;
+  const int blk = PAIR ? (i16 >> 3) : 0, el = PAIR ? (i16 & 7) : i16;  // this lane's row and entry
+  const int dme = (PAIR && blk) ? dB : dA;
   float ce = 0.f, we = 0.f;
-  if (i16 < d) rating_weights(r, a.implicit, a.alpha, ce, we);
-  const bool valid = i16 < d && ce > 0.f;
-  const int npos = a.implicit ? __popcll(__ballot(i16 < d && r > 0.f) & 0xFFFFull) : d;
-  const float lamn = a.reg * (float)npos;
+  if (el < dme) rating_weights(r, a.implicit, a.alpha, ce, we);
+  const bool valid = el < dme && ce > 0.f;
+  const uint64_t pos = __ballot(el < dme && r > 0.f);
+  const int nposA = a.implicit ? __popcll(pos & (PAIR ? 0xFFull : 0xFFFFull)) : dA;
+  const int nposB = a.implicit ? __popcll(pos & 0xFF00ull) : dB;
+  const float lamnA = a.reg * (float)nposA, lamnB = a.reg * (float)nposB;
 
-  // D^-1/2 (lane: columns lane + 64h) and one power-of-two scale for the whole row's fp16 operands
-  float sd[NHC];
+  // D^-1/2 per row (lane: columns lane + 64h) and one power-of-two scale for the unit's fp16 operands
+  float sdA[NHC], sdB[NHC];
   bool bad = false;
   float bnd = 0.f;
 #pragma unroll
   for (int h = 0; h < NHC; ++h) {
     const int cc = lane + 64 * h;
-    const float dd = s_lam[cc] + lamn;
-    if (cc < a.kreal && !(dd > 0.f)) bad = true;
-    sd[h] = (cc < a.kreal && dd > 0.f) ? frsq(dd) : 0.f;
-    bnd = fmaxf(bnd, sd[h] * s_csi[cc]);
+    const float lm = s_lam[cc], cs = s_csi[cc];
+    const float ddA = lm + lamnA;
+    if (cc < a.kreal && !(ddA > 0.f)) bad = true;
+    sdA[h] = (cc < a.kreal && ddA > 0.f) ? frsq(ddA) : 0.f;
+    bnd = fmaxf(bnd, sdA[h] * cs);
+    if constexpr (PAIR) {
+      const float ddB = lm + lamnB;
+      if (dB > 0 && cc < a.kreal && !(ddB > 0.f)) bad = true;
+      sdB[h] = (cc < a.kreal && ddB > 0.f) ? frsq(ddB) : 0.f;
+      if (dB > 0) bnd = fmaxf(bnd, sdB[h] * cs);
+    }
   }
   bnd = wave_max(bnd);
   int ex = 0;
   frexpf(bnd * 8192.f, &ex);  // max |z_c · sd_c| < 2^13 · bnd < 2^ex
   const float sc = ldexpf(1.f, 13 - ex), usc = ldexpf(1.f, 2 * (ex - 13));
 #pragma unroll
-  for (int h = 0; h < NHC; ++h) sdl[lane + 64 * h] = sd[h] * sc;
+  for (int h = 0; h < NHC; ++h) {
+    sdlA[lane + 64 * h] = sdA[h] * sc;
+    if constexpr (PAIR) sdlB[lane + 64 * h] = sdB[h] * sc;
+  }
   WAVE_LDS_SYNC();
+  const float* sdl = (PAIR && blk) ? sdlB : sdlA;  // this lane's row
 
   // S = Zs Zsᵀ on split-fp16 MFMA (hi·hi + hi·lo + lo·hi); both operands are Zs, so the 32 k-slots
   // of step q may take columns 32q + 4g .. +3 and 32q + 16 + 4g .. +3
@@ -129,11 +150,14 @@ __device__ __forceinline__ void light16_row(const SolveArgs& a, int j, int d, fl
   }
   acc *= usc;
   // K = S + C⁻¹ (identity rows for masked / absent entries): lane (i16, g) holds K[4g + r][i16],
-  // the diagonal is entry i16's own
+  // the diagonal is entry i16's own; PAIR: the cross block between the two rows is dropped
   const float cinv = valid ? frcp(ce) : 0.f;
   const float dadd = valid ? cinv : 1.0f;
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) acc[rr] += (4 * g + rr == i16) ? dadd : 0.f;
+  for (int rr = 0; rr < 4; ++rr) {
+    acc[rr] += (4 * g + rr == i16) ? dadd : 0.f;
+    if constexpr (PAIR) acc[rr] = ((4 * g + rr) >> 3) == blk ? acc[rr] : 0.f;
+  }
   if (__any(bad) && lane == 0) atomicOr(a.err, 1);
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) st[(4 * g + rr) * L16_LDK + i16] = acc[rr];
@@ -145,22 +169,25 @@ __device__ __forceinline__ void light16_row(const SolveArgs& a, int j, int d, fl
 #pragma unroll
     for (int e = 0; e < 4; ++e) kr[4 * u + e] = v[e];
   }
+  // live column c: an entry of its row (c < dA, or PAIR: block B's c - 8 < dB)
+  auto live = [&](int c) { return PAIR ? (c < 8 ? c < dA : c - 8 < dB) : c < dA; };
 
-  // Cholesky K = L Lᵀ over the d live columns (lane i holds row i: kr[m] = L[i][m], m <= i), with the
+  // Cholesky K = L Lᵀ over the live columns (lane i holds row i: kr[m] = L[i][m], m <= i), with the
   // forward substitution L y = C⁻¹ w in the same steps; broadcasts of lane c by DPP row_newbcast
   float y = valid ? we * cinv : 0.f, dg = 1.f;
   bool notpd = false;
   static_for<0, 16>([&](auto cc) {
     constexpr int c = decltype(cc)::value;
-    if (c >= d) return;
+    constexpr int cend = (PAIR && c < 8) ? 8 : 16;  // PAIR: the other block's rows are untouched
+    if (!live(c)) return;
     const float piv = bc16_after_asm<c>(kr[c]);
     if (!(piv > 0.f)) notpd = true;
     const float inv = frsq(piv), s = piv * inv;
     kr[c] = (i16 == c) ? s : kr[c] * inv;
     dg = (i16 == c) ? inv : dg;
-    static_for<c + 1, 16>([&](auto mm) {
+    static_for<c + 1, cend>([&](auto mm) {
       constexpr int m = decltype(mm)::value;
-      if (m >= d) return;
+      if (!live(m)) return;
       fnmac_bc16<m, m == c + 1>(kr[m], kr[c], kr[c]);
     });
     const float yc = bc16<c>(y * dg);
@@ -179,16 +206,18 @@ __device__ __forceinline__ void light16_row(const SolveArgs& a, int j, int d, fl
   for (int m = 0; m < 16; ++m) lt[m] = st[m * L16_LDK + i16];  // L[m][i16] (m >= i16 used)
   static_for<0, 16>([&](auto cc) {
     constexpr int c = 15 - decltype(cc)::value;
-    if (c >= d) return;
+    if (!live(c)) return;
     const float vc = bc16<c>(y * dg);
     y = (i16 < c) ? fmaf(-lt[c], vc, y) : ((i16 == c) ? vc : y);
   });
   if (g == 0) vsh[i16] = y;  // v (zero for masked / absent entries)
 
   // x' = D⁻¹ Zᵀ v through the stage: 64 columns per pass; lane l sums columns 2(l & 31), +1 over the
-  // entries 8(l >> 5) + u (u < min(8, d)), the two halves meet by one cross-half shuffle
+  // entries 8(l >> 5) + u.  Single row: u < min(8, d), the two halves meet by one cross-half shuffle;
+  // PAIR: half 0 is row A, half 1 row B (u < max(dA, dB): absent entries are zero rows with v = 0).
   const int eh = lane >> 5, cl = 2 * (lane & 31);
-  const int nu = d < 8 ? d : 8;
+  const int nu = PAIR ? (dA > dB ? dA : dB) : (dA < 8 ? dA : 8);
+  const float* sdo = (PAIR && eh) ? sdlB : sdlA;
 #pragma unroll
   for (int h = 0; h < KP / L16_COLS; ++h) {
     WAVE_LDS_SYNC();  // previous reads of the scratch / stage done
@@ -202,28 +231,32 @@ __device__ __forceinline__ void light16_row(const SolveArgs& a, int j, int d, fl
       const f32x2 z2 = *reinterpret_cast<const f32x2*>(st + e * L16_SLD + cl);
       xa += z2 * vsh[e];
     }
-    xa[0] += __shfl_xor(xa[0], 32);
-    xa[1] += __shfl_xor(xa[1], 32);
-    // D⁻¹ = (sd·sc)² / sc² (exact power-of-two rescaling); lanes of half 0 hold the columns, the
-    // caller stores them once the next row's loads are issued
-    const f32x2 s2 = *reinterpret_cast<const f32x2*>(sdl + L16_COLS * h + cl);
+    if constexpr (!PAIR) {
+      xa[0] += __shfl_xor(xa[0], 32);
+      xa[1] += __shfl_xor(xa[1], 32);
+    }
+    // D⁻¹ = (sd·sc)² / sc² (exact power-of-two rescaling); the caller stores them once the next
+    // unit's loads are issued
+    const f32x2 s2 = *reinterpret_cast<const f32x2*>(sdo + L16_COLS * h + cl);
     xo[h] = xa * (s2 * s2 * usc);
   }
 }
 
-// Persistent waves over the row list (row i of the wave: wave id + i·waves), software-pipelined so
-// that one dependent memory latency per row remains exposed instead of four (rows -> ptr -> col/val
-// -> Z).  Row descriptors {row, p0, degree} (a.desc) come by scalar loads two rows ahead; the next
-// row's (col, val) entries are in flight while the current row computes; the Z gather of the next
-// row is issued as soon as the current row's registers are free.  No vector load in the pipeline is
+// Persistent waves over the unit list (unit i of the wave: wave id + i·waves), software-pipelined so
+// that one dependent memory latency per unit remains exposed instead of four (rows -> ptr -> col/val
+// -> Z).  Row descriptors {row, p0, degree} (a.desc) come by scalar loads two units ahead; the next
+// unit's (col, val) entries are in flight while the current one computes; the Z gather of the next
+// unit is issued as soon as the current unit's registers are free.  No vector load in the pipeline is
 // conditional (masked entries read index 0 / gather the zero row a.zero_row), so the waits count only
 // what they need; Λ and the column scales are staged in LDS once per workgroup.
-template <int KP>
+// PAIR: unit u = rows 2u and 2u + 1 of the list (degree <= 8 each).
+template <int KP, bool PAIR>
 __global__ __launch_bounds__(256, KP <= 128 ? 5 : 4) void solve_light16_kernel(SolveArgs a) {
   constexpr int NC = KP / 16, WF = l16_wave_floats(KP);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, i16 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int blk = PAIR ? (i16 >> 3) : 0, el = PAIR ? (i16 & 7) : i16;
   float* s_lam = smem + 4 * WF;  // [KP] Λ, then [KP] inverse column scales
   float* s_csi = s_lam + KP;
   for (int e = threadIdx.x; e < KP; e += 256) {
@@ -231,61 +264,74 @@ __global__ __launch_bounds__(256, KP <= 128 ? 5 : 4) void solve_light16_kernel(S
     s_csi[e] = a.colscale[KP + e];
   }
   __syncthreads();  // the only workgroup barrier
-  float* st = smem + wave * WF;    // K / L scratch, then the x' stage
-  float* sdl = st + 16 * L16_SLD;  // D^-1/2 · sc per column
-  float* vsh = sdl + KP;           // v
-  const int64_t n = a.n_rows, nw = (int64_t)gridDim.x * 4;
-  int64_t ridx = (int64_t)blockIdx.x * 4 + wave;
-  if (ridx >= n) return;
+  float* st = smem + wave * WF;     // K / L scratch, then the x' stage
+  float* sdlA = st + 16 * L16_SLD;  // D^-1/2 · sc per column, row A
+  float* vsh = sdlA + KP;           // v
+  float* sdlB = vsh + 16;           // row B (PAIR)
+  const int64_t n = a.n_rows, nu_ = PAIR ? (n + 1) / 2 : n, nw = (int64_t)gridDim.x * 4;
+  int64_t uidx = (int64_t)blockIdx.x * 4 + wave;
+  if (uidx >= nu_) return;
   auto desc = [&](int64_t i) {  // constant address space: a wave-uniform index becomes s_load_dwordx4
+    if (i >= n) return int4{0, 0, 0, 0};
     typedef __attribute__((address_space(4))) const int cint;
     cint* q = (cint*)(a.desc) + 4 * i;
     return int4{q[0], q[1], q[2], q[3]};
   };
-  auto entries = [&](const int4& dd, float& rr, int& cc) {
+  struct Unit { int4 a, b; };  // row descriptors; b is zero without a second row
+  auto unit = [&](int64_t u) {
+    if (u >= nu_) return Unit{int4{0, 0, 0, 0}, int4{0, 0, 0, 0}};
+    if constexpr (PAIR) return Unit{desc(2 * u), desc(2 * u + 1)};
+    else return Unit{desc(u), int4{0, 0, 0, 0}};
+  };
+  auto entries = [&](const Unit& U, float& rr, int& cc) {
+    const int4& dd = (PAIR && blk) ? U.b : U.a;
     const int64_t p0 = (int64_t)(uint32_t)dd.y | ((int64_t)dd.z << 32);
-    const int64_t e = i16 < dd.w ? p0 + i16 : 0;  // unconditional load (index 0 always exists)
+    const int64_t e = el < dd.w ? p0 + el : 0;  // unconditional load (index 0 always exists)
     rr = a.val[e];
     cc = a.col[e];
   };
   f32x4 zf[NC];
-  auto gather = [&](float rr, int cc, int dd) {
-    const int64_t src = entry_valid(a, rr, i16, dd) ? cc : a.zero_row;
+  auto gather = [&](const Unit& U, float rr, int cc) {
+    const int dd = (PAIR && blk) ? U.b.w : U.a.w;
+    const int64_t src = entry_valid(a, rr, el, dd) ? cc : a.zero_row;
 #pragma unroll
     for (int c = 0; c < NC; ++c) zf[c] = ld4(a.Z + src * KP + 16 * c + 4 * g);
   };
-  int4 dA = desc(ridx);
-  float r, rN = 0.f;
-  int colE, cN = 0;
-  entries(dA, r, colE);
-  gather(r, colE, dA.w);
-  int4 dB = ridx + nw < n ? desc(ridx + nw) : int4{0, 0, 0, 0};
-  entries(dB, rN, cN);
-  int4 dC = ridx + 2 * nw < n ? desc(ridx + 2 * nw) : int4{0, 0, 0, 0};
-  const int cl = 2 * (lane & 31);
-  auto store = [&](int j, const f32x2 (&xo)[KP / L16_COLS]) {
-    if (lane < 32) {
+  const int eh = lane >> 5, cl = 2 * (lane & 31);
+  auto store = [&](const Unit& U, const f32x2 (&xo)[KP / L16_COLS]) {
+    // single row: half 0 holds the columns; PAIR: half 0 row A, half 1 row B (if present)
+    const int j = (PAIR && eh) ? U.b.x : U.a.x;
+    const bool on = PAIR ? (eh == 0 || U.b.w > 0) : lane < 32;
+    if (on) {
 #pragma unroll
       for (int h = 0; h < KP / L16_COLS; ++h) *reinterpret_cast<f32x2*>(a.X + (int64_t)j * KP + L16_COLS * h + cl) = xo[h];
     }
   };
+  Unit uA = unit(uidx);
+  float r, rN = 0.f;
+  int colE, cN = 0;
+  entries(uA, r, colE);
+  gather(uA, r, colE);
+  Unit uB = unit(uidx + nw);
+  entries(uB, rN, cN);
+  Unit uC = unit(uidx + 2 * nw);
   for (;;) {
     f32x2 xo[KP / L16_COLS];
-    light16_row<KP>(a, dA.x, dA.w, r, colE, zf, st, sdl, vsh, s_lam, s_csi, xo);
-    const int jdone = dA.x;
-    ridx += nw;
-    if (ridx >= n) {
-      store(jdone, xo);
+    light16_unit<KP, PAIR>(a, uA.a.w, uA.b.w, r, colE, zf, st, sdlA, sdlB, vsh, s_lam, s_csi, xo);
+    const Unit done = uA;
+    uidx += nw;
+    if (uidx >= nu_) {
+      store(done, xo);
       break;
     }
-    dA = dB;
-    dB = dC;
+    uA = uB;
+    uB = uC;
     r = rN;
     colE = cN;
-    gather(r, colE, dA.w);
-    entries(dB, rN, cN);  // row ridx + nw (dB is zero past the end: a harmless load of index 0)
-    store(jdone, xo);     // after the loads: the next waits do not cover these stores
-    dC = ridx + 2 * nw < n ? desc(ridx + 2 * nw) : int4{0, 0, 0, 0};
+    gather(uA, r, colE);
+    entries(uB, rN, cN);  // unit uidx + nw (zero descriptors past the end: harmless loads of index 0)
+    store(done, xo);      // after the loads: the next waits do not cover these stores
+    uC = unit(uidx + 2 * nw);
   }
 }
 
@@ -300,18 +346,24 @@ __global__ void row_desc_kernel(const int32_t* __restrict__ rows, int64_t n, con
 
 }  // namespace
 
-hipError_t launch_solve_light16(int KP, const SolveArgs& a, hipStream_t s) {
+// pair = true: the rows (all of degree <= 8) are solved two per unit
+hipError_t launch_solve_light16(int KP, const SolveArgs& a, hipStream_t s, bool pair) {
   if (a.n_rows <= 0) return hipSuccess;
   if (!a.desc || a.n_cu <= 0) return hipErrorInvalidValue;
   const int per_cu = KP <= 128 ? 5 : 4;  // resident workgroups per CU (launch bounds)
-  const int64_t need = (a.n_rows + 3) / 4;
+  const int64_t units = pair ? (a.n_rows + 1) / 2 : a.n_rows;
+  const int64_t need = (units + 3) / 4;
   const int blocks = (int)std::min<int64_t>(need, (int64_t)a.n_cu * per_cu);
   const size_t lds = ((size_t)4 * l16_wave_floats(KP) + 2 * KP) * sizeof(float);
-  if (KP == 64) solve_light16_kernel<64><<<blocks, 256, lds, s>>>(a);
-  else if (KP == 128) solve_light16_kernel<128><<<blocks, 256, lds, s>>>(a);
-  else if (KP == 256) solve_light16_kernel<256><<<blocks, 256, lds, s>>>(a);
-  else return hipErrorInvalidValue;
-  return hipGetLastError();
+#define L16(kp)                                                                  \
+  if (KP == kp) {                                                                \
+    if (pair) solve_light16_kernel<kp, true><<<blocks, 256, lds, s>>>(a);        \
+    else solve_light16_kernel<kp, false><<<blocks, 256, lds, s>>>(a);            \
+    return hipGetLastError();                                                    \
+  }
+  L16(64) L16(128) L16(256)
+#undef L16
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_row_desc(const int32_t* rows, int64_t n, const int64_t* ptr, int32_t* desc, hipStream_t s) {
