@@ -349,7 +349,7 @@ __device__ __forceinline__ void light_row(const SolveArgs& a, int j, int d, floa
       const int cc = lane + 64 * h;
       bnd = fmaxf(bnd, sdl[cc] * a.colscale[KP + cc]);
     }
-    for (int o = 32; o > 0; o >>= 1) bnd = fmaxf(bnd, __shfl_xor(bnd, o));
+    bnd = wave_max_dpp(bnd);
     int ex = 0;
     frexpf(bnd * 8192.f, &ex);  // bnd·2^13 < 2^ex
     const float sc = ldexpf(1.f, 13 - ex), usc = ldexpf(1.f, 2 * (ex - 13));

@@ -72,6 +72,19 @@ __device__ __forceinline__ float rows4_sum(float x) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// max over the wave of a non-negative value, in every lane: DPP row_shr prefix maxima within the
+// 16-lane rows, row_bcast:15 / :31 across rows (lane 63 ends with the maximum), then readlane -- VALU
+// only (a __shfl_xor butterfly is six dependent LDS round trips)
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x118, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xF, 0xF, false)));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
 // v_rsq_f32 / v_rcp_f32 / v_sqrt_f32: single instructions (~1 ulp) instead of the IEEE-exact
 // multi-instruction expansions; the solve tolerance is 1e-4 relative (tests state it)
 __device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }

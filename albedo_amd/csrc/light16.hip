@@ -57,21 +57,6 @@ __device__ __forceinline__ void split8(f32x4 a, f32x4 b, f16x8& hi, f16x8& lo) {
   lo = __builtin_bit_cast(f16x8, (u32x4{lw[0], lw[1], lw[2], lw[3]}));
 }
 
-// max over the wave of a non-negative value, in every lane: DPP row_shr prefix maxima within the
-// 16-lane rows, row_bcast:15 / :31 across rows (lane 63 ends with the maximum), then readlane
-__device__ __forceinline__ float wave_max(float v) {
-  auto dpp = [](float x, auto ctrl) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), decltype(ctrl)::value, 0xF, 0xF, false));
-  };
-  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x111>{}));
-  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x112>{}));
-  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x114>{}));
-  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x118>{}));
-  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x142>{}));
-  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x143>{}));
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
-
 // entry i16 of a light row counts (Spark masks c = 0 ratings out of A and b)
 __device__ __forceinline__ bool entry_valid(const SolveArgs& a, float r, int i16, int d) {
   float ce, we;
@@ -122,7 +107,7 @@ __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB,
       if (dB > 0) bnd = fmaxf(bnd, sdB[h] * cs);
     }
   }
-  bnd = wave_max(bnd);
+  bnd = wave_max_dpp(bnd);
   int ex = 0;
   frexpf(bnd * 8192.f, &ex);  // max |z_c · sd_c| < 2^13 · bnd < 2^ex
   const float sc = ldexpf(1.f, 13 - ex), usc = ldexpf(1.f, 2 * (ex - 13));
