@@ -45,19 +45,10 @@ struct WaveRow {
   static constexpr int NI = SPS / RPI;                   // DMA instructions per stage
   static constexpr int STAGE = SPS * RB + 64 * (SPS / 8 - 1);  // + 64 B per 8-rating group (banks)
   static constexpr int WAVES = 4;                        // rows per workgroup (independent waves)
-  static constexpr int STAGE_AL = (STAGE + 255) & ~255;
-  static constexpr int SCR = 2048;                       // factor / b' scratch, apart from the stage
-  static constexpr int LDS_WAVE = STAGE_AL + SCR;        // the stage can take the next row's DMA
+  static constexpr int LDS_WAVE = (STAGE + 255) & ~255;
   static constexpr int LDS = WAVES * LDS_WAVE + 2 * KP * 4;  // + column scales and inverses
   static_assert(RPI * RB == 1024 && 8 % RPI == 0, "DMA pieces never cross an 8-rating group");
-  static_assert(2 * LDS <= 160 * 1024, "two workgroups per CU");
-};
-
-// The first stage of a wave's next row, issued while the current row factors (its indices and the
-// (col, val) registers the build loop continues from)
-struct WavePf {
-  int c_cur, c_nxt;
-  float r_cur, r_nxt;
+  static_assert(LDS_WAVE >= 2048 + NQ * 1024, "the stage doubles as the factor's scratch + L⁻¹ store");
 };
 
 // LDS byte offset of (rating r of the stage, column c).  Lane i + 16q reads ratings 8q..8q+7 of
@@ -81,15 +72,9 @@ __device__ __forceinline__ f16x4v tr_read(const char* p) {
 // the CSR, gathered 32 per stage into this wave's LDS stage st.  On return acc holds the NT upper
 // tiles of Σ c·(cs z)(cs z)ᵀ (still column-scaled), bacc[A] (lane i + 16q) b'[16A + i] unscaled;
 // returns the number of positive ratings.
-// pin: the first stage of this row was issued by the previous row's build (its registers); nd > 0: the
-// row np0 / nd comes next on this wave -- its first stage is issued into st as soon as this row's last
-// fragments are in registers (pout receives its registers), so the stage fills while this row
-// factors.  scr: this wave's scratch apart from the stage (the b' transposition).
 template <int KP, bool IMPLICIT, bool PRE>
-__device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d, char* st, float* scr, const float* s_cs,
-                                          f32x4 (&acc)[WaveRow<KP>::NT], float (&bacc)[WaveRow<KP>::NQ],
-                                          const WavePf* pin = nullptr, int64_t np0 = 0, int nd = 0,
-                                          WavePf* pout = nullptr) {
+__device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d, char* st, const float* s_cs,
+                                          f32x4 (&acc)[WaveRow<KP>::NT], float (&bacc)[WaveRow<KP>::NQ]) {
   using W = WaveRow<KP>;
   constexpr int NQ = W::NQ, NT = W::NT;
   const int lane = threadIdx.x & 63, q = lane >> 4, i16 = lane & 15;
@@ -103,19 +88,17 @@ __device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d,
   for (int e = 0; e < CPL; ++e) bpart[e] = 0.f;
   int npos = 0;
 
-  // (col, val) of stage s of the row at rp0 / rd: lane l holds rating 32 s + (l & 31), clamped to the
-  // row (zero weight)
-  auto iload_of = [&](int64_t rp0, int rd, int s, int& c_out, float& r_out) {
+  // (col, val) of stage s: lane l holds rating 32 s + (l & 31), clamped to the row (zero weight)
+  auto iload = [&](int s, int& c_out, float& r_out) {
     const int e = W::SPS * s + (lane & 31);
-    const int64_t pe = rp0 + (e < rd ? e : rd - 1);
+    const int64_t pe = p0 + (e < d ? e : d - 1);
     c_out = a.col[pe];
     r_out = a.val[pe];
     if constexpr (PRE) {  // past the row end: the zero row (its products vanish in A' and b')
-      c_out = e < rd ? c_out : (int)a.zero_row;
-      r_out = e < rd ? r_out : 0.f;
+      c_out = e < d ? c_out : (int)a.zero_row;
+      r_out = e < d ? r_out : 0.f;
     }
   };
-  auto iload = [&](int s, int& c_out, float& r_out) { iload_of(p0, d, s, c_out, r_out); };
   // gather of one stage: piece u holds ratings RPI·u .. RPI·u + RPI-1, lane l the 16 B at
   // 4·(l % LPR) of rating RPI·u + l / LPR; the rating's src row is wave-uniform (readlane)
   auto dma = [&](int cidx) {
@@ -150,26 +133,11 @@ __device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d,
     r_cur = r_nxt;
     if (s + 2 < nst) iload(s + 2, c_nxt, r_nxt);
   };
-  if (pin) {
-    c_cur = pin->c_cur;
-    c_nxt = pin->c_nxt;
-    r_cur = pin->r_cur;
-    r_nxt = pin->r_nxt;
-  } else if (nst > 0) {
+  if (nst > 0) {
     iload(0, c_cur, r_cur);
     dma(c_cur);
     if (nst > 1) iload(1, c_nxt, r_nxt);
   }
-  // after the last stage's fragments: the next row's first stage into the (now free) stage
-  auto prefetch_next = [&]() {
-    if (nd <= 0) return;
-    WavePf& o = *pout;
-    iload_of(np0, nd, 0, o.c_cur, o.r_cur);
-    dma(o.c_cur);
-    o.c_nxt = 0;
-    o.r_nxt = 0.f;
-    if (nd > W::SPS) iload_of(np0, nd, 1, o.c_nxt, o.r_nxt);
-  };
   f32x4 bt = zero4();  // PRE: b' of every block in one tile (column 2A: w hi, 2A + 1: w lo)
   for (int s = 0; s < nst; ++s) {
     const bool in = W::SPS * s + (lane & 31) < d;
@@ -219,7 +187,6 @@ __device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d,
       }
       WAVE_LDS_SYNC();
       if (s + 1 < nst) next_stage(s);
-      else prefetch_next();
       __builtin_amdgcn_sched_barrier(0);
       static_for<0, NQ>([&](auto AA) {
         constexpr int A = decltype(AA)::value;
@@ -271,7 +238,6 @@ __device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d,
       }
       WAVE_LDS_SYNC();
       if (s + 1 < nst) next_stage(s);
-      else prefetch_next();
       __builtin_amdgcn_sched_barrier(0);
       static_for<0, NQ>([&](auto AA) {
         static_for<decltype(AA)::value, NQ>([&](auto BB) {
@@ -285,7 +251,7 @@ __device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d,
   __builtin_amdgcn_sched_barrier(0);  // keep the factor's loads out of the build loop
   // ---- b' complete (sum over the four rating groups), tiles unscaled, diagonal Λ + λn ----------
   // b' to the factor's layout (lane i + 16q holds b'[16A + i] for every block A) through LDS
-  float* bsc = scr;
+  float* bsc = reinterpret_cast<float*>(st);
   if constexpr (PRE) {  // bt: lane j + 16q holds column j (block j >> 1, w hi / lo), rows 4q .. 4q+3
 #pragma unroll
     for (int r = 0; r < 4; ++r) bsc[16 * i16 + 4 * q + r] = bt[r];
