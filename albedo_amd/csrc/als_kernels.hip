@@ -1275,6 +1275,315 @@ __device__ __forceinline__ bool nnls_stop(double step, double ndir, double nx) {
   return isnan(step) || step < 1e-7 || step > 1e40 || ndir < 1e-12 * nx || ndir < 1e-32;
 }
 
+// ---- NNLS iteration on a register-resident A (KP = 128 / 256) --------------------------------
+// The workgroup's NW waves hold A once per row: wave w = (is, js) keeps the 4 x 4 tiles of row blocks
+// 4is .. 4is+3 and column blocks 4js .. 4js+3, lane i + 16q the entries A[16I + 4q + r][16J + i]
+// (64 floats, as 32 fp32 pairs for v_pk_fma_f32).  A·g is then 32 packed FMAs on the four g[16J + i]
+// a lane needs (one ds_read_b128) and a 15-step recursive-halving sum over the lane's 16-lane DPP row
+// (row_mirror, row_half_mirror, quad reversal, quad swap: partners i^15, i^7, i^3, i^1).  Each lane
+// stores its 16 row partials in a lane-dependent slot order s -> k = s ^ m(i) (m linear over GF(2),
+// m(15) = 8, m(7) = 4, m(3) = 2, m(1) = 1) so that the half a lane keeps and the half its partner sends
+// sit in the same registers: no selects.  Lane i ends with row 16(4is + (m(i) >> 2)) + 4q + (m(i) & 3)
+// summed over its column-block set; the waves with js = 0 own those rows (x, residual, directions and
+// A·dir in fp64).
+// Spark's iteration needs A·g and A·dir, dir = g + alpha·lastDir.  By linearity A·dir = A·g +
+// alpha·A·lastDir, and A·lastDir is the previous step's A·dir (kept by the owner), so ONE product per
+// iteration suffices; the owner forms dir, ‖dir‖², dir·res and the wall ratios in fp64 as Spark does,
+// and dir·A·dir = g·A·g + 2 alpha g·(A lastDir) + alpha² lastDir·A·lastDir (the last term is the
+// previous step's curvature).  Two barriers per iteration: (B1) the owners publish g (fp32) and the
+// sums ‖g‖², g·res, ‖x‖², wall hits, g·A·lastDir; (B2) every wave publishes its row partials of A·g and
+// of g·A·g, the owners ‖dir‖², dir·res and the two wall-ratio minima.  Only the owner waves evaluate the
+// step and the stopping rule; the others learn a stop at the next pass's first barrier (LDS flag).
+__device__ __forceinline__ int nnls_slot_mask(int i) {
+  return ((i & 1) ? 1 : 0) ^ ((i & 2) ? 3 : 0) ^ ((i & 4) ? 6 : 0) ^ ((i & 8) ? 12 : 0);
+}
+__device__ __forceinline__ double rdlane_d(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+// a wave-uniform double into scalar registers (the VALU results of uniform math stay in VGPRs otherwise)
+__device__ __forceinline__ double uni(double v) {
+  return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)), __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
+__device__ __forceinline__ double vmin_f64(double a, double b) {  // no NaN canonicalisation (none occur)
+  double r;
+  asm volatile("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// DPP move of a double with bound_ctrl (lanes without a source read 0)
+template <int CTRL>
+__device__ __forceinline__ double dpp64z(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+// sum over each 16-lane row (row_shr prefix), the result in the row's lane 15
+__device__ __forceinline__ double row16_sum(double x) {
+  x += dpp64z<0x111>(x);
+  x += dpp64z<0x112>(x);
+  x += dpp64z<0x114>(x);
+  x += dpp64z<0x118>(x);
+  return x;
+}
+// min over each 16-lane row, the result in the row's lane 15 (lanes without a source keep their own)
+__device__ __forceinline__ double row16_min(double x) {
+  x = vmin_f64(x, dpp64<0x111, 0xF>(x, x));
+  x = vmin_f64(x, dpp64<0x112, 0xF>(x, x));
+  x = vmin_f64(x, dpp64<0x114, 0xF>(x, x));
+  x = vmin_f64(x, dpp64<0x118, 0xF>(x, x));
+  return x;
+}
+// (u, w) -> lanes of one half / row set hold u's pair sum, the others w's: v_permlane32_swap (halves)
+// or v_permlane16_swap (odd rows of u with even rows of w)
+template <bool R32, bool MIN>
+__device__ __forceinline__ double halve64(double u, double w) {
+  const auto lo = R32 ? __builtin_amdgcn_permlane32_swap(__double2loint(u), __double2loint(w), false, false)
+                      : __builtin_amdgcn_permlane16_swap(__double2loint(u), __double2loint(w), false, false);
+  const auto hi = R32 ? __builtin_amdgcn_permlane32_swap(__double2hiint(u), __double2hiint(w), false, false)
+                      : __builtin_amdgcn_permlane16_swap(__double2hiint(u), __double2hiint(w), false, false);
+  const double a = __hiloint2double((int)hi[0], (int)lo[0]), b = __hiloint2double((int)hi[1], (int)lo[1]);
+  return MIN ? vmin_f64(a, b) : a + b;
+}
+// Wave reduction of 8 values (slots 0, 2, 4, 6 summed, 1, 3, 5, 7 minimised): halves by permlane32
+// (k, k+4), rows by permlane16 (k, k+2), then row prefixes.  Value n ends in lane 15 of row
+// r(n) = 2 (n >> 2) + ((n >> 1) & 1), slot n & 1 of the returned pair.
+__device__ __forceinline__ void wave_reduce8(const double (&x)[8], double& s, double& m) {
+  const double y0 = halve64<true, false>(x[0], x[4]), y2 = halve64<true, false>(x[2], x[6]);
+  const double y1 = halve64<true, true>(x[1], x[5]), y3 = halve64<true, true>(x[3], x[7]);
+  s = row16_sum(halve64<false, false>(y0, y2));
+  m = row16_min(halve64<false, true>(y1, y3));
+}
+
+template <int KP>
+struct NnlsReg {
+  static constexpr int NB = KP / 16, NW = Heavy<KP>::NW, IB = 4, JB = 4, NIS = NB / IB, NJS = NB / JB;
+  static_assert(NIS * NJS == NW && NW <= 16, "one wave per (row-block set, column-block set)");
+  // LDS, inside the tile area once A is in registers (floats)
+  static constexpr int OFF_G = 0;                      // fp32 g, element c at (c & 15)·NB + (c >> 4)
+  static constexpr int OFF_P = OFF_G + KP;             // row partials of A·g [NJS][KP]
+  static constexpr int OFF_R1 = OFF_P + NJS * KP;      // fp64 wave partials of B1 [8][16]
+  static constexpr int OFF_R2 = OFF_R1 + 2 * 128;      // fp64 wave partials of B2 [8][16]
+  static constexpr int OFF_FLAG = OFF_R2 + 2 * 128;    // stop flag
+  static constexpr int FLOATS = OFF_FLAG + 4;
+  static_assert(FLOATS <= (KP / 16) * (KP / 16 + 1) / 2 * 256, "fits the dead tile area");
+};
+
+__device__ __forceinline__ int nnls_vidx(int c, int NB) { return (c & 15) * NB + (c >> 4); }
+
+template <int KP>
+__device__ void nnls_reg_iterate(const SolveArgs& a, float* smem, int j, int iter_max) {
+  using R = NnlsReg<KP>;
+  using H = Heavy<KP>;
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  constexpr int NB = R::NB, NIS = R::NIS, NW = R::NW;
+  const float* bvec = smem + H::OFF_B;
+  int* s_flag = reinterpret_cast<int*>(smem + H::OFF_FLAG);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, q = lane >> 4;
+  const int is = wave % NIS, js = wave / NIS;
+  const bool own = js == 0;  // wave-uniform
+  const int msk = nnls_slot_mask(i16);
+  const int c_own = 16 * (R::IB * is + (msk >> 2)) + 4 * q + (msk & 3);
+  // A into registers: slot s (pair s & 7, half s >> 3) holds row k = s ^ msk of the lane's 16
+  f2 av[8][4];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int k = s ^ msk;
+    const int row = 16 * (R::IB * is + (k >> 2)) + 4 * q + (k & 3);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int col = 16 * (R::JB * js + jj) + i16;
+      av[s & 7][jj][s >> 3] = smem[row >= col ? nel(row, col) : nel(col, row)];
+    }
+  }
+  const float bi = own ? bvec[c_own] : 0.f;
+  __syncthreads();  // the tile area is free from here on
+  float* sG = smem + R::OFF_G;
+  float* sP = smem + R::OFF_P;
+  double* sR1 = reinterpret_cast<double*>(smem + R::OFF_R1);
+  double* sR2 = reinterpret_cast<double*>(smem + R::OFF_R2);
+  int* sStop = reinterpret_cast<int*>(smem + R::OFF_FLAG);
+  const int vrow = i16 * NB + R::JB * js;  // this lane's product columns in sG
+  const int vown = nnls_vidx(c_own, NB);
+  // A·v over the lane's columns, summed over the 16-lane row: the partial of row c_own
+  auto product = [&](const f32x4 v) -> float {
+    f2 p[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      p[s] = av[s][0] * f2{v[0], v[0]};
+      p[s] = av[s][1] * f2{v[1], v[1]} + p[s];
+      p[s] = av[s][2] * f2{v[2], v[2]} + p[s];
+      p[s] = av[s][3] * f2{v[3], v[3]} + p[s];
+    }
+    float h[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) h[s] = p[s][0] + dppf<0x140>(p[s][1]);  // row_mirror: lane i^15
+#pragma unroll
+    for (int s = 0; s < 4; ++s) h[s] += dppf<0x141>(h[s + 4]);  // row_half_mirror: lane i^7
+#pragma unroll
+    for (int s = 0; s < 2; ++s) h[s] += dppf<0x1B>(h[s + 2]);  // quad_perm [3,2,1,0]: lane i^3
+    return h[0] + dppf<0xB1>(h[1]);                             // quad_perm [1,0,3,2]: lane i^1
+  };
+  // owner state (fp64); uniform: last_norm, the previous step's ‖dir‖² and dir·A·dir
+  double xi = 0.0, axi = 0.0, last_dir = 0.0, a_last = 0.0;
+  float hit = 0.f;
+  double last_norm = 0.0, last_dad = 0.0;
+  // owner waves, per pass: B1's totals and the CG direction
+  double ngrad = 0.0, gres = 0.0, nx = 0.0, gal = 0.0, alpha = 0.0, dc = 0.0;
+  bool cg = false;
+  int last_wall = 0, iterno = 0;
+  bool stopped = false;  // owner waves only (the others learn it at the next barrier)
+  if (tid == 0) sStop[0] = 0;
+  NNLS_T0();
+  for (; iterno < iter_max; ++iterno) {
+    if (iterno > 0 && (iterno & 63) == 0) {  // exact residual refresh: A·x
+      if (own && !stopped) sG[vown] = (float)xi;
+      if (tid == 0) sStop[0] = stopped;
+      __syncthreads();
+      if (sStop[0]) break;
+      sP[js * KP + c_own] = product(ld4(sG + vrow));
+      __syncthreads();
+      if (own) {
+        float y = sP[c_own];
+#pragma unroll
+        for (int w = 1; w < R::NJS; ++w) y += sP[w * KP + c_own];
+        axi = (double)y;
+      }
+    }
+    // residual = A x - b ; projected gradient
+    const double res = own ? axi - (double)bi : 0.0;
+    double gi = res;
+    if (gi > 0.0 && xi == 0.0) gi = 0.0;
+    if (own && !stopped) {
+      // sums in slots 0, 2, 4, 6: ‖g‖², g·res, ‖x‖², g·A·lastDir; slot 1: wall hits (max = min of -hit)
+      const double t[8] = {gi * gi, -(double)hit, gi * res, INFINITY, xi * xi, INFINITY, gi * a_last, INFINITY};
+      double s, m;
+      wave_reduce8(t, s, m);
+      if ((lane & 15) == 15) {
+        const int r = lane >> 4;  // row r: value 4 (r >> 1) + 2 (r & 1) in s, the next one in m
+        const int n = 4 * (r >> 1) + 2 * (r & 1);
+        sR1[n * 16 + is] = s;
+        sR1[(n + 1) * 16 + is] = m;
+      }
+      sG[vown] = (float)gi;
+    }
+    if (tid == 0) sStop[0] = stopped;
+    NNLS_PH(0);
+    __syncthreads();  // B1
+    NNLS_PH(1);
+    if (sStop[0]) break;
+    // the product A·g (every wave), its row partial to LDS
+    const float gc = sG[vown];
+    const float p0 = product(ld4(sG + vrow));
+    sP[js * KP + c_own] = p0;
+    double t_gag = (double)gc * (double)p0;
+    NNLS_PH(2);
+    if (own) {
+      // r1 totals: lane l reads value l >> 4 (t0) and 4 + (l >> 4) (t1) of wave l & 15; rows 0, 2 of
+      // each register are sums, rows 1, 3 minima
+      {
+        const bool wv = (lane & 15) < NIS;
+        const bool mn = (lane >> 4) & 1;
+        const double z = mn ? INFINITY : 0.0;
+        double t0 = wv ? sR1[lane] : z;
+        double t1 = wv ? sR1[64 + lane] : z;
+        t0 = mn ? row16_min(t0) : row16_sum(t0);
+        t1 = mn ? row16_min(t1) : row16_sum(t1);
+        ngrad = rdlane_d(t0, 15);
+        gres = rdlane_d(t0, 47);
+        nx = rdlane_d(t1, 15);
+        gal = rdlane_d(t1, 47);
+        if (-rdlane_d(t0, 31) > 0.0) last_wall = iterno - 1;  // the previous step's wall hits
+      }
+      cg = iterno > last_wall + 1;
+      alpha = cg ? uni(ngrad / last_norm) : 0.0;
+      dc = cg ? gi + alpha * last_dir : 0.0;
+      // sums: g·A·g partials, ‖dir‖², dir·res; minima: wall ratios of g and of dir
+      const double t[8] = {t_gag, gi > 0.0 ? xi / gi : INFINITY, dc * dc, (cg && dc > 0.0) ? xi / dc : INFINITY,
+                           dc * res, INFINITY, 0.0, INFINITY};
+      double s, m;
+      wave_reduce8(t, s, m);
+      if ((lane & 15) == 15) {
+        const int r = lane >> 4;
+        const int n = 4 * (r >> 1) + 2 * (r & 1);
+        sR2[n * 16 + wave] = s;
+        sR2[(n + 1) * 16 + wave] = m;
+      }
+    } else {
+      t_gag = row16_sum(t_gag);
+      t_gag += dpp64z<0x142>(t_gag);  // row_bcast:15
+      t_gag += dpp64z<0x143>(t_gag);  // row_bcast:31 -> lane 63
+      if (lane == 63) sR2[wave] = t_gag;
+    }
+    NNLS_PH(3);
+    __syncthreads();  // B2
+    NNLS_PH(4);
+    if (own) {
+      double s0, s1;
+      {
+        // value n = lane >> 4 of register 0 (sum / min by row parity), value 4 + (lane >> 4) of register 1
+        const bool wv = (lane & 15) < NW;
+        const int n0 = lane >> 4;
+        const bool ownv = (lane & 15) < NIS;  // only owner waves wrote values 1 .. 7
+        const double z = (n0 & 1) ? INFINITY : 0.0;
+        s0 = (n0 == 0 ? wv : ownv) ? sR2[lane] : z;
+        s1 = ownv ? sR2[64 + lane] : z;
+        s0 = (n0 & 1) ? row16_min(s0) : row16_sum(s0);
+        s1 = (n0 & 1) ? row16_min(s1) : row16_sum(s1);
+      }
+      const double gag = rdlane_d(s0, 15), mg = rdlane_d(s0, 31), ndc = rdlane_d(s0, 47), md = rdlane_d(s0, 63);
+      const double dres = rdlane_d(s1, 15);
+      float y0 = sP[c_own];
+#pragma unroll
+      for (int w = 1; w < R::NJS; ++w) y0 += sP[w * KP + c_own];
+      const double agi = (double)y0;
+      double step = gres / (gag + 1e-20);
+      double di = gi, adi = agi, ndir = ngrad, dad_used = gag;
+      bool use_dc = false;
+      if (cg) {
+        const double dad = gag + 2.0 * alpha * gal + alpha * alpha * last_dad;
+        const double dstep = dres / (dad + 1e-20);
+        if (!nnls_stop(dstep, ndc, nx)) {  // else: reject the CG direction
+          step = dstep;
+          di = dc;
+          adi = agi + alpha * a_last;
+          ndir = ndc;
+          dad_used = dad;
+          use_dc = true;
+        }
+      }
+      if (nnls_stop(step, ndir, nx)) {
+        stopped = true;
+      } else {
+        // don't run through the walls
+        step = fmin(step, use_dc ? md : mg);
+        // take the step
+        hit = 0.f;
+        if (step * di > xi * (1 - 1e-14)) {
+          xi = 0.0;
+          hit = 1.f;
+        } else {
+          xi -= step * di;
+        }
+        axi -= step * adi;
+        last_dir = di;
+        a_last = adi;
+        last_dad = uni(dad_used);
+      }
+      last_norm = ngrad;
+    }
+    NNLS_PH(5);
+    if (stopped) continue;  // owner waves: on to the next pass's first barrier, which ends the loop
+  }
+  NNLS_OUT();
+  // iterations in Spark's count: the pass whose stopping rule fired (the loop ran one pass further)
+  if (stopped) --iterno;
+  if (own) a.X[(int64_t)j * KP + c_own] = c_own < a.kreal ? (float)xi : 0.f;
+  if (tid == 0 && s_flag[1]) atomicOr(a.err, s_flag[1]);
+  if (tid == 0 && a.iters) {
+    atomicAdd(&a.iters[0], (unsigned long long)iterno);
+    atomicMax(&a.iters[1], (unsigned long long)iterno);
+  }
+}
+
 // NNLS rows (nonnegative = true; Spark NNLSSolver -> mllib/optimization/NNLS.scala).  Original basis
 // (the constraints are coordinate-wise): A = G + λn I + Σ c y yᵀ built like the heavy rows (same LDS
 // stage + MFMA) into the NNLS tile layout, then Spark's projected gradient with CG acceleration:
@@ -1283,7 +1592,7 @@ __device__ __forceinline__ bool nnls_stop(double step, double ndir, double nx) {
 // alpha·lastDir is known once ‖grad‖² is reduced), and the residual follows the steps
 // (A·x_new = A·x - step·A·dir, exact refresh every 64 iterations): Spark's three products become one
 // pass.  Stopping rules, the wall clamp and the CG restarts are Spark's, unchanged.
-template <int KP, bool PRE = false>
+template <int KP, bool PRE = false, bool REG = false>
 __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a, const float* __restrict__ Gt) {
   using H = Heavy<KP>;
   using NL = NnlsLds<KP>;
@@ -1322,6 +1631,11 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
   for (int e = tid; e < NTT; e += NTH) smem[e] += Gt[e];  // A = G + Σ c y yᵀ (Gt: the same layout)
   __syncthreads();
   for (int c = tid; c < KP; c += NTH) smem[nel(c, c)] += c < a.kreal ? lamn : 1.0f;
+  if constexpr (REG) {
+    __syncthreads();
+    nnls_reg_iterate<KP>(a, smem, j, 400 > 20 * a.kreal ? 400 : 20 * a.kreal);
+    return;
+  }
   const bool own = tid < KP;
   const int i = own ? tid : 0;
   const double bi = own ? (double)bvec[i] : 0.0;
@@ -1418,15 +1732,24 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
 template <int KP>
 hipError_t launch_nnls_kp(const SolveArgs& a, const float* Gt, hipStream_t s) {
   const size_t lds = NnlsLds<KP>::FLOATS * 4;
+  // KP >= 128: A in registers (nnls_reg_iterate); ALBEDO_NNLS_REG=0 keeps the LDS-streamed loop
+  constexpr bool CAN_REG = KP >= 128;
+  static const bool reg = CAN_REG && !(getenv("ALBEDO_NNLS_REG") && atoi(getenv("ALBEDO_NNLS_REG")) == 0);
   static const hipError_t attr = allow_lds(solve_nnls_kernel<KP, false>, lds);
   static const hipError_t attr2 = allow_lds(solve_nnls_kernel<KP, true>, lds);
+  static const hipError_t attr3 = allow_lds(solve_nnls_kernel<KP, false, CAN_REG>, lds);
+  static const hipError_t attr4 = allow_lds(solve_nnls_kernel<KP, true, CAN_REG>, lds);
   if (attr != hipSuccess) return attr;
   if (attr2 != hipSuccess) return attr2;
+  if (attr3 != hipSuccess) return attr3;
+  if (attr4 != hipSuccess) return attr4;
   // one workgroup per row, in launches of at most 2^31 work-items (an AQL dispatch's grid size is a
   // 32-bit work-item count: 4.9M rows x 1024 threads would wrap and silently drop rows)
   for (int64_t r0 = 0; r0 < a.n_rows; r0 += max_rows_per_launch(Heavy<KP>::NTH)) {
     SolveArgs b = chunk_args(a, r0, Heavy<KP>::NTH, SplitRec<KP>::FLOATS);
-    if (b.prebuilt) solve_nnls_kernel<KP, true><<<(int)b.n_rows, Heavy<KP>::NTH, lds, s>>>(b, Gt);
+    if (reg && b.prebuilt) solve_nnls_kernel<KP, true, CAN_REG><<<(int)b.n_rows, Heavy<KP>::NTH, lds, s>>>(b, Gt);
+    else if (reg) solve_nnls_kernel<KP, false, CAN_REG><<<(int)b.n_rows, Heavy<KP>::NTH, lds, s>>>(b, Gt);
+    else if (b.prebuilt) solve_nnls_kernel<KP, true><<<(int)b.n_rows, Heavy<KP>::NTH, lds, s>>>(b, Gt);
     else solve_nnls_kernel<KP, false><<<(int)b.n_rows, Heavy<KP>::NTH, lds, s>>>(b, Gt);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
