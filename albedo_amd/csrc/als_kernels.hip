@@ -1324,12 +1324,22 @@ __device__ __forceinline__ double row16_sum(double x) {
   x += dpp64z<0x118>(x);
   return x;
 }
-// min over each 16-lane row, the result in the row's lane 15 (lanes without a source keep their own)
-__device__ __forceinline__ double row16_min(double x) {
-  x = vmin_f64(x, dpp64<0x111, 0xF>(x, x));
-  x = vmin_f64(x, dpp64<0x112, 0xF>(x, x));
-  x = vmin_f64(x, dpp64<0x114, 0xF>(x, x));
-  x = vmin_f64(x, dpp64<0x118, 0xF>(x, x));
+// sum or min over each 16-lane row, the result in every lane of the row: butterfly over the lane
+// partners i^15, i^7, i^3, i^1 (row_mirror, row_half_mirror, quad perms) -- every lane has a source,
+// so no fill values and no bound_ctrl; partners combine the same operands (bit-identical results)
+template <int CTRL>
+__device__ __forceinline__ double dpp64f(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+template <bool MIN>
+__device__ __forceinline__ double row16_all(double x) {
+  auto op = [](double a, double b) { return MIN ? vmin_f64(a, b) : a + b; };
+  x = op(x, dpp64f<0x140>(x));
+  x = op(x, dpp64f<0x141>(x));
+  x = op(x, dpp64f<0x1B>(x));
+  x = op(x, dpp64f<0xB1>(x));
   return x;
 }
 // (u, w) -> lanes of one half / row set hold u's pair sum, the others w's: v_permlane32_swap (halves)
@@ -1343,14 +1353,14 @@ __device__ __forceinline__ double halve64(double u, double w) {
   const double a = __hiloint2double((int)hi[0], (int)lo[0]), b = __hiloint2double((int)hi[1], (int)lo[1]);
   return MIN ? vmin_f64(a, b) : a + b;
 }
-// Wave reduction of 8 values (slots 0, 2, 4, 6 summed, 1, 3, 5, 7 minimised): halves by permlane32
-// (k, k+4), rows by permlane16 (k, k+2), then row prefixes.  Value n ends in lane 15 of row
-// r(n) = 2 (n >> 2) + ((n >> 1) & 1), slot n & 1 of the returned pair.
+// Wave reduction of 4 sums (x[0..3]) and 4 minima (x[4..7]): halves by permlane32 (k, k+2), rows by
+// permlane16 (k, k+1), then a row butterfly.  Sum k ends in every lane of row
+// r = 2 (k >> 1) + (k & 1) of s, minimum k in the same row of m.
 __device__ __forceinline__ void wave_reduce8(const double (&x)[8], double& s, double& m) {
-  const double y0 = halve64<true, false>(x[0], x[4]), y2 = halve64<true, false>(x[2], x[6]);
-  const double y1 = halve64<true, true>(x[1], x[5]), y3 = halve64<true, true>(x[3], x[7]);
-  s = row16_sum(halve64<false, false>(y0, y2));
-  m = row16_min(halve64<false, true>(y1, y3));
+  const double y0 = halve64<true, false>(x[0], x[2]), y1 = halve64<true, false>(x[1], x[3]);
+  const double z0 = halve64<true, true>(x[4], x[6]), z1 = halve64<true, true>(x[5], x[7]);
+  s = row16_all<false>(halve64<false, false>(y0, y1));
+  m = row16_all<true>(halve64<false, true>(z0, z1));
 }
 
 template <int KP>
@@ -1453,15 +1463,13 @@ __device__ void nnls_reg_iterate(const SolveArgs& a, float* smem, int j, int ite
     double gi = res;
     if (gi > 0.0 && xi == 0.0) gi = 0.0;
     if (own && !stopped) {
-      // sums in slots 0, 2, 4, 6: ‖g‖², g·res, ‖x‖², g·A·lastDir; slot 1: wall hits (max = min of -hit)
-      const double t[8] = {gi * gi, -(double)hit, gi * res, INFINITY, xi * xi, INFINITY, gi * a_last, INFINITY};
+      // sums ‖g‖², g·res, ‖x‖², g·A·lastDir; minimum -hit (the previous step's wall hits)
+      const double t[8] = {gi * gi, gi * res, xi * xi, gi * a_last, -(double)hit, INFINITY, INFINITY, INFINITY};
       double s, m;
       wave_reduce8(t, s, m);
-      if ((lane & 15) == 15) {
-        const int r = lane >> 4;  // row r: value 4 (r >> 1) + 2 (r & 1) in s, the next one in m
-        const int n = 4 * (r >> 1) + 2 * (r & 1);
-        sR1[n * 16 + is] = s;
-        sR1[(n + 1) * 16 + is] = m;
+      if ((lane & 15) == 0) {  // row r holds sum r and minimum r
+        sR1[q * 16 + is] = s;
+        sR1[64 + q * 16 + is] = m;
       }
       sG[vown] = (float)gi;
     }
@@ -1479,33 +1487,27 @@ __device__ void nnls_reg_iterate(const SolveArgs& a, float* smem, int j, int ite
     if (own) {
       // r1 totals: lane l reads value l >> 4 (t0) and 4 + (l >> 4) (t1) of wave l & 15; rows 0, 2 of
       // each register are sums, rows 1, 3 minima
-      {
+      {  // lane l: sum / minimum l >> 4 of owner wave l & 15
         const bool wv = (lane & 15) < NIS;
-        const bool mn = (lane >> 4) & 1;
-        const double z = mn ? INFINITY : 0.0;
-        double t0 = wv ? sR1[lane] : z;
-        double t1 = wv ? sR1[64 + lane] : z;
-        t0 = mn ? row16_min(t0) : row16_sum(t0);
-        t1 = mn ? row16_min(t1) : row16_sum(t1);
-        ngrad = rdlane_d(t0, 15);
-        gres = rdlane_d(t0, 47);
-        nx = rdlane_d(t1, 15);
-        gal = rdlane_d(t1, 47);
-        if (-rdlane_d(t0, 31) > 0.0) last_wall = iterno - 1;  // the previous step's wall hits
+        const double t0 = row16_all<false>(wv ? sR1[lane] : 0.0);
+        const double t1 = row16_all<true>(wv ? sR1[64 + lane] : INFINITY);
+        ngrad = rdlane_d(t0, 0);
+        gres = rdlane_d(t0, 16);
+        nx = rdlane_d(t0, 32);
+        gal = rdlane_d(t0, 48);
+        if (-rdlane_d(t1, 0) > 0.0) last_wall = iterno - 1;  // the previous step's wall hits
       }
       cg = iterno > last_wall + 1;
       alpha = cg ? uni(ngrad / last_norm) : 0.0;
       dc = cg ? gi + alpha * last_dir : 0.0;
       // sums: g·A·g partials, ‖dir‖², dir·res; minima: wall ratios of g and of dir
-      const double t[8] = {t_gag, gi > 0.0 ? xi / gi : INFINITY, dc * dc, (cg && dc > 0.0) ? xi / dc : INFINITY,
-                           dc * res, INFINITY, 0.0, INFINITY};
+      const double t[8] = {t_gag, dc * dc, dc * res, 0.0, gi > 0.0 ? xi / gi : INFINITY,
+                           (cg && dc > 0.0) ? xi / dc : INFINITY, INFINITY, INFINITY};
       double s, m;
       wave_reduce8(t, s, m);
-      if ((lane & 15) == 15) {
-        const int r = lane >> 4;
-        const int n = 4 * (r >> 1) + 2 * (r & 1);
-        sR2[n * 16 + wave] = s;
-        sR2[(n + 1) * 16 + wave] = m;
+      if ((lane & 15) == 0) {
+        sR2[q * 16 + wave] = s;
+        sR2[64 + q * 16 + wave] = m;
       }
     } else {
       t_gag = row16_sum(t_gag);
@@ -1518,19 +1520,13 @@ __device__ void nnls_reg_iterate(const SolveArgs& a, float* smem, int j, int ite
     NNLS_PH(4);
     if (own) {
       double s0, s1;
-      {
-        // value n = lane >> 4 of register 0 (sum / min by row parity), value 4 + (lane >> 4) of register 1
-        const bool wv = (lane & 15) < NW;
-        const int n0 = lane >> 4;
-        const bool ownv = (lane & 15) < NIS;  // only owner waves wrote values 1 .. 7
-        const double z = (n0 & 1) ? INFINITY : 0.0;
-        s0 = (n0 == 0 ? wv : ownv) ? sR2[lane] : z;
-        s1 = ownv ? sR2[64 + lane] : z;
-        s0 = (n0 & 1) ? row16_min(s0) : row16_sum(s0);
-        s1 = (n0 & 1) ? row16_min(s1) : row16_sum(s1);
+      {  // lane l: sum / minimum l >> 4 of wave l & 15 (sum 0 from every wave, the rest from the owners)
+        const bool ownv = (lane & 15) < NIS;
+        s0 = row16_all<false>(((q == 0 ? (lane & 15) < NW : ownv)) ? sR2[lane] : 0.0);
+        s1 = row16_all<true>(ownv ? sR2[64 + lane] : INFINITY);
       }
-      const double gag = rdlane_d(s0, 15), mg = rdlane_d(s0, 31), ndc = rdlane_d(s0, 47), md = rdlane_d(s0, 63);
-      const double dres = rdlane_d(s1, 15);
+      const double gag = rdlane_d(s0, 0), ndc = rdlane_d(s0, 16), dres = rdlane_d(s0, 32);
+      const double mg = rdlane_d(s1, 0), md = rdlane_d(s1, 16);
       float y0 = sP[c_own];
 #pragma unroll
       for (int w = 1; w < R::NJS; ++w) y0 += sP[w * KP + c_own];
