@@ -64,10 +64,12 @@ struct NBatch {
   static constexpr int RT = SV >= 4 ? SV / 4 : 1;    // refill when this many slots are idle
   // LDS, in floats
   static constexpr int OFF_Y = 0;                            // [SV][YS]
-  static constexpr int OFF_V = SV * YS;                      // [2 vectors][hi|lo][NS][4][16][8] halves
-  static constexpr int OFF_P = OFF_V + 2 * KP * S;           // [2][NW][SV][DLP]: Ỹv partials
-  static constexpr int OFF_U = OFF_P + 2 * NW * SV * DLP;     // [2][SV][DLP]: Ỹv per slot
-  static constexpr int OFF_R = (OFF_U + 2 * SV * DLP + 3) & ~3;  // doubles [2][NW][16][8]
+  static constexpr int OFF_V = SV * YS;                      // [hi|lo][NS][4][16][8] halves
+  static constexpr int OFF_P = OFF_V + KP * S;               // [NW][SV][DLP]: Ỹv partials
+  static constexpr int OFF_U = OFF_P + NW * SV * DLP;        // [SV][DLP]: Ỹv per slot
+  static constexpr int AS = KP + 4;                          // A·lastDir row stride (banks)
+  static constexpr int OFF_A = OFF_U + SV * DLP;             // [SV][AS]: A·lastDir per slot (fp32)
+  static constexpr int OFF_R = (OFF_A + SV * AS + 3) & ~3;   // doubles [2][NW][16][8]
   static constexpr int OFF_C = OFF_R + 2 * 2 * NW * S * 8;      // ints
   static constexpr int FLOATS = OFF_C + 4;
   static_assert(NW * RBW == NQ && NQ % 2 == 0 && RBW <= 2, "row blocks split evenly over the waves");
@@ -147,6 +149,7 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
   int j = lane & 15, g = lane >> 4;
   bool slot_lane = j < SV;                          // columns past SV stay empty
   float* Yj = smem + NB::OFF_Y + (slot_lane ? j : 0) * YS;  // this lane's slot
+  float* Aj = smem + NB::OFF_A + (slot_lane ? j : 0) * NB::AS;  // its A·lastDir (fp32)
   double* R = reinterpret_cast<double*>(smem + NB::OFF_R);
   int* ctl = reinterpret_cast<int*>(smem + NB::OFF_C);
   _Float16* Vh = reinterpret_cast<_Float16*>(smem + NB::OFF_V);
@@ -183,6 +186,7 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
   // of v_n for the fp16 split; lamn = λn (1 on pad coordinates)
   auto product = [&](auto NVV, const float (*vin)[RBW][4], const float* vs, float (*yout)[RBW][4], float lamn) {
     constexpr int NV = decltype(NVV)::value;
+    static_assert(NV == 1, "the V / P / U buffers hold one vector");
     // B fragments: coordinate 32 s + 8 gg + h of slot j at hi/lo [((s·4 + gg)·16 + j)·8 + h]
 #pragma unroll
     for (int n = 0; n < NV; ++n) {
@@ -314,11 +318,13 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
   };
 
   // slot state (every lane of a slot holds the slot's scalars)
+  // ald = A·lastDir: A·dir = A·g + alpha·A·lastDir (linearity), so one product per iteration
+  // (ald in fp32: it is an fp32 product's value carried forward, the registers go to the products)
   double x[RBW][4], ax[RBW][4], ld[RBW][4];
   float bb[RBW][4];
   bool act = false;
   int row = 0, iterno = 0, last_wall = 0, npos = 0, dd = 0;
-  double last_norm = 0.0, hit = 0.0, last_dmax = 0.0;
+  double last_norm = 0.0, hit = 0.0, last_dad = 0.0;
   const int iter_max = 400 > 20 * a.kreal ? 400 : 20 * a.kreal;
   bool exhausted = false;
   int wg_iter = 0;
@@ -331,6 +337,7 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
       g = (ot >> 4) & 3;
       slot_lane = j < SV;
       Yj = smem + NB::OFF_Y + (slot_lane ? j : 0) * YS;
+      Aj = smem + NB::OFF_A + (slot_lane ? j : 0) * NB::AS;
     }
     // ---- refill idle slots (uniform: every wave sees the same slot flags) ----------------------
     const unsigned idle = (unsigned)__ballot(slot_lane && !act) & ((1u << SV) - 1u);
@@ -376,11 +383,15 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
 #pragma unroll
           for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
-            for (int t = 0; t < 4; ++t) x[rb][t] = ax[rb][t] = ld[rb][t] = 0.0;
+            for (int t = 0; t < 4; ++t) {
+              x[rb][t] = ax[rb][t] = ld[rb][t] = 0.0;
+            }
+#pragma unroll
+          for (int rb = 0; rb < RBW; ++rb) *reinterpret_cast<f32x4*>(Aj + 16 * (w * RBW + rb) + 4 * g) = zero4();
           iterno = 0;
           last_wall = 0;
           last_norm = 0.0;
-          last_dmax = 0.0;
+          last_dad = 0.0;
           hit = 0.0;
         }
       }
@@ -401,7 +412,7 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
           xin[0][rb][t] = (float)x[rb][t];
           xm[0] = fmax(xm[0], fabs(x[rb][t]));
         }
-      slot_reduce(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, xm, 0, 5);
+      slot_reduce(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, xm, 0, 6);
       const float vs[1] = {pow2_scale(xm[0])};
       product(std::integral_constant<int, 1>{}, xin, vs, yo, lamn);
 #pragma unroll
@@ -417,7 +428,7 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
       const double res = ax[rb][t] - (double)bb[rb][t];
       return (res > 0.0 && x[rb][t] == 0.0) ? 0.0 : res;
     };
-    double r1[5] = {0.0, 0.0, 0.0, hit, 0.0};  // Σg², Σg·res, Σx², wall hits | max|g|
+    double r1[6] = {0.0, 0.0, 0.0, hit, 0.0, 0.0};  // Σg², Σg·res, Σx², wall hits, Σg·A·lastDir | max|g|
 #pragma unroll
     for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
@@ -427,34 +438,33 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
         r1[0] += gv * gv;
         r1[1] += gv * res;
         r1[2] += x[rb][t] * x[rb][t];
-        r1[4] = fmax(r1[4], fabs(gv));
+        r1[4] += gv * (double)Aj[16 * (w * RBW + rb) + 4 * g + t];
+        r1[5] = fmax(r1[5], fabs(gv));
       }
-    slot_reduce(std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{}, r1, 0, 0);
+    slot_reduce(std::integral_constant<int, 5>{}, std::integral_constant<int, 1>{}, r1, 0, 0);
     BT_PH(2);
     if (r1[3] > 0.0) last_wall = iterno - 1;
     const double ngrad = r1[0], nx = r1[2];
     const bool cg = iterno > last_wall + 1;
     const double alpha = cg ? ngrad / last_norm : 0.0;
 
-    // ---- A·grad and A·dir --------------------------------------------------------------------------
-    float vin[2][RBW][4], yo[2][RBW][4];
+    // ---- A·grad (A·dir = A·grad + alpha·A·lastDir) --------------------------------------------------
+    float vin[1][RBW][4], yo[1][RBW][4];
 #pragma unroll
     for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const double gv = grad(rb, t);
-        vin[0][rb][t] = (float)gv;
-        vin[1][rb][t] = cg ? (float)(gv + alpha * ld[rb][t]) : 0.f;
-      }
-    // max|dir| <= max|g| + |alpha| max|last dir| (one bit of slack at most)
-    const float vs[2] = {pow2_scale(r1[4]), pow2_scale(r1[4] + fabs(alpha) * last_dmax)};
-    product(std::integral_constant<int, 2>{}, vin, vs, yo, lamn);
+      for (int t = 0; t < 4; ++t) vin[0][rb][t] = (float)grad(rb, t);
+    const float vs[1] = {pow2_scale(r1[5])};
+    product(std::integral_constant<int, 1>{}, vin, vs, yo, lamn);
     BT_PH(5);
-    // Σg·Ag, Σd·res, Σd·Ad, Σd² | max|d|, and the wall ratios of both candidate directions:
-    // -min x_i/g_i over g_i > 0, -min x_i/d_i over d_i > 0 (Spark clamps the step to the smallest
-    // x_i/dir_i below it; the minimum over every positive dir_i gives the same clamp, so the ratio
-    // rides in this reduction instead of a third one after the direction is chosen)
-    double r2[7] = {0.0, 0.0, 0.0, 0.0, 0.0, -INFINITY, -INFINITY};
+    // Σg·Ag, Σd·res, Σd² | and the wall ratios of both candidate directions: -min x_i/g_i over
+    // g_i > 0, -min x_i/d_i over d_i > 0 (Spark clamps the step to the smallest x_i/dir_i below it;
+    // the minimum over every positive dir_i gives the same clamp, so the ratio rides in this
+    // reduction instead of a third one after the direction is chosen).  d·Ad = g·Ag + 2 alpha
+    // g·A·lastDir + alpha² lastDir·A·lastDir (the previous step's curvature).
+    // (the lane's smallest ratios are selected by cross-multiplication, then divided once each)
+    double r2[5] = {0.0, 0.0, 0.0, -INFINITY, -INFINITY};
+    double ng = 0.0, dg = 0.0, nd = 0.0, ddn = 0.0;  // numerator / denominator of the lane's minima
 #pragma unroll
     for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
@@ -464,40 +474,50 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
         const double dc = cg ? gv + alpha * ld[rb][t] : 0.0;
         r2[0] += gv * (double)yo[0][rb][t];
         r2[1] += dc * res;
-        r2[2] += dc * (double)yo[1][rb][t];
-        r2[3] += dc * dc;
-        r2[4] = fmax(r2[4], fabs(dc));
-        if (gv > 0.0) r2[5] = fmax(r2[5], -(x[rb][t] / gv));
-        if (dc > 0.0) r2[6] = fmax(r2[6], -(x[rb][t] / dc));
+        r2[2] += dc * dc;
+        if (gv > 0.0 && (dg == 0.0 || x[rb][t] * dg < ng * gv)) {
+          ng = x[rb][t];
+          dg = gv;
+        }
+        if (dc > 0.0 && (ddn == 0.0 || x[rb][t] * ddn < nd * dc)) {
+          nd = x[rb][t];
+          ddn = dc;
+        }
       }
-    slot_reduce(std::integral_constant<int, 4>{}, std::integral_constant<int, 3>{}, r2, 1, 0);
+    if (dg > 0.0) r2[3] = -(ng / dg);
+    if (ddn > 0.0) r2[4] = -(nd / ddn);
+    slot_reduce(std::integral_constant<int, 3>{}, std::integral_constant<int, 2>{}, r2, 1, 0);
     BT_PH(6);
-    double step = r1[1] / (r2[0] + 1e-20), ndir = ngrad;
+    double step = r1[1] / (r2[0] + 1e-20), ndir = ngrad, dad_used = r2[0];
     bool use_dc = false;
     if (cg) {
-      const double dstep = r2[1] / (r2[2] + 1e-20);
-      if (!stop_rule(dstep, r2[3], nx)) {  // else: reject the CG direction
+      const double dad = r2[0] + 2.0 * alpha * r1[4] + alpha * alpha * last_dad;
+      const double dstep = r2[1] / (dad + 1e-20);
+      if (!stop_rule(dstep, r2[2], nx)) {  // else: reject the CG direction
         step = dstep;
-        ndir = r2[3];
+        ndir = r2[2];
+        dad_used = dad;
         use_dc = true;
       }
     }
     const bool stop = !act || stop_rule(step, ndir, nx);
     // don't run through the walls
-    step = fmin(step, -(use_dc ? r2[6] : r2[5]));
+    step = fmin(step, -(use_dc ? r2[4] : r2[3]));
     BT_PH(7);
     bool finish = act && stop;
     if (act && !stop) {
       hit = 0.0;
 #pragma unroll
-      for (int rb = 0; rb < RBW; ++rb)
+      for (int rb = 0; rb < RBW; ++rb) {
+        float* ap = Aj + 16 * (w * RBW + rb) + 4 * g;
+        const f32x4 a4 = ld4(ap);
+        f32x4 an;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const double gv = grad(rb, t);
           const double di = use_dc ? gv + alpha * ld[rb][t] : gv;
-          float y0v = yo[0][rb][t], y1v = yo[1][rb][t];
-          asm("" : "+v"(y0v), "+v"(y1v));  // a select of values, not of array slots (scratch)
-          const double adi = (double)(use_dc ? y1v : y0v);
+          const double agi = (double)yo[0][rb][t];
+          const double adi = use_dc ? agi + alpha * (double)a4[t] : agi;
           if (step * di > x[rb][t] * (1 - 1e-14)) {
             x[rb][t] = 0.0;
             hit = 1.0;
@@ -506,9 +526,12 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
           }
           ax[rb][t] -= step * adi;
           ld[rb][t] = di;
+          an[t] = (float)adi;
         }
+        if (slot_lane) *reinterpret_cast<f32x4*>(ap) = an;
+      }
       last_norm = ngrad;
-      last_dmax = use_dc ? r2[4] : r1[4];
+      last_dad = dad_used;
       ++iterno;
       finish = iterno >= iter_max;
     }
@@ -538,7 +561,7 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
           bb[rb][t] = 0.f;
         }
       hit = 0.0;
-      last_dmax = 0.0;
+      last_dad = 0.0;
     }
     BT_PH(8);
   }
