@@ -163,6 +163,7 @@ struct als_ctx {
   DevBuf slab, d_G, d_P, d_lam, d_err, d_Gt, d_cs, d_csmax;
   DevBuf d_partial, d_reduced;   // split-K partial / reduced A' records (shared by both sides)
   DevBuf d_Zhl;                  // pre-split src rows of the uniform-confidence heavy build
+  DevBuf d_Pf;                   // P's bf16 parts in MFMA fragment order (rotate_bf)
   DevBuf d_iters;                // NNLS iteration counters (sum, max)
   DevBuf d_gfrag, d_counter;     // lockstep NNLS: G in MFMA operand order, row counter
   int n_cu = 256;
@@ -171,7 +172,7 @@ struct als_ctx {
   int64_t topk_stats[4] = {0, 0, 0, 0};
   std::vector<int32_t> last_rescan;  // src ids the last als_recommend sent to the exact rescan
   int split_len = 0;             // ratings per split-K chunk (0: no split)
-  std::vector<float> h_P32, h_lam32, h_Gt;  // host staging of async H2D copies (outlive the sync)
+  std::vector<float> h_P32, h_lam32, h_Gt, h_ub;  // host staging of async H2D copies (outlive the sync)
   int slab_blocks = 0;
   hipEvent_t ev[8] = {};
   hipStream_t st2 = nullptr;     // world > 1: factor-chunk gathers behind the solve
@@ -637,23 +638,44 @@ int column_scales(als_ctx* c, const Side& S, const Side& T, bool have_max = fals
 int heavy_launches(als_ctx* c, const Side& T, SolveArgs a, int64_t h0, int64_t hn, bool nnls, int q = 0);
 bool use_wave_kernel(const als_ctx* c);
 
+// KP = 128: the rotation on bf16 MFMA with the fused operand split (rotate_bf); ALBEDO_ROTATE_BF=0
+// keeps the fp32 MFMA rotation + colmax epilogue + separate presplit pass (A/B)
+bool rotate_bf_on(const als_ctx* c) {
+  static const bool off = [] {
+    const char* e = std::getenv("ALBEDO_ROTATE_BF");
+    return e && std::atoi(e) == 0;
+  }();
+  return !off && c->KP == 128;
+}
+
 // One confidence c for every rating of dst side T (explicit: c = 1; implicit: all |r| equal): the
 // heavy build's operand split z·√c·colscale -> fp16 hi + lo is then the same for every gather of a
 // src row, so it runs once per src row here (launch_presplit) instead of once per gathered rating
 // inside the wave kernel.  ALBEDO_PRESPLIT=0 keeps the per-rating split (A/B).
-int presplit(als_ctx* c, const Side& S, const Side& T, const void** zhl, float* wsc, float* inv_sw) {
+// presplit_wanted: whether the split applies to this half (and its √c); split_done: the rotation
+// already wrote it (rotate_bf)
+bool presplit_wanted(const als_ctx* c, const Side& T, float* sw) {
   static const bool off = [] {
     const char* e = std::getenv("ALBEDO_PRESPLIT");
     return e && std::atoi(e) == 0;
   }();
-  *zhl = nullptr;
   const bool uniform = !c->p.implicit_prefs || (T.vmin == T.vmax && T.vmax > 0.f);
-  if (off || !uniform || !use_wave_kernel(c) || T.boff[NBUCKET] == T.boff[B_HEAVY]) return ALS_OK;
+  if (off || !uniform || !use_wave_kernel(c) || T.boff[NBUCKET] == T.boff[B_HEAVY]) return false;
   const float cw = c->p.implicit_prefs ? (float)c->p.alpha * T.vmax : 1.0f;
-  if (!(cw > 0.f)) return ALS_OK;
-  const float sw = std::sqrt(cw);
+  if (!(cw > 0.f)) return false;
+  *sw = std::sqrt(cw);
+  return true;
+}
+
+int presplit(als_ctx* c, const Side& S, const Side& T, const void** zhl, float* wsc, float* inv_sw,
+             bool split_done = false) {
+  *zhl = nullptr;
+  float sw = 1.f;
+  if (!presplit_wanted(c, T, &sw)) return ALS_OK;
+  const float cw = c->p.implicit_prefs ? (float)c->p.alpha * T.vmax : 1.0f;
   HIPCHK(c->d_Zhl.ensure((size_t)(S.prows() + 1) * c->KP * 4));
-  HIPCHK(launch_presplit(c->KP, S.d_Z.as<float>(), S.prows(), c->d_cs.as<float>(), sw, c->d_Zhl.p, c->st));
+  if (!split_done)
+    HIPCHK(launch_presplit(c->KP, S.d_Z.as<float>(), S.prows(), c->d_cs.as<float>(), sw, c->d_Zhl.p, c->st));
   // b' weights w = 1 + c (implicit, r > 0) or r (explicit), scaled by a power of two below 2^13
   const double wmax = c->p.implicit_prefs ? 1.0 + (double)cw : (double)T.vmax;
   int e = 0;
@@ -825,7 +847,7 @@ int half_sweep(als_ctx* c, int t) {
   hipEvent_t* ev = c->ev;
   const bool multi = c->world > 1;
   double eig_ms = 0.0;
-  bool have_cmax = false;
+  bool have_cmax = false, cs_done = false, split_done = false;
   bool force_heavy = c->p.light_max_degree == 0;
   // world > 1: the previous half's factor gathers (second stream) finish before any collective or
   // rotation of this one is issued -- two RCCL operations of one communicator must never overlap
@@ -887,13 +909,32 @@ int half_sweep(als_ctx* c, int t) {
     HIPCHK(hipMemcpyAsync(c->d_P.p, P32.data(), P32.size() * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(c->d_lam.p, lam32.data(), lam32.size() * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(ev[2], st));
-    // world > 1: every rank rotates the whole gathered src (no collective on the critical path);
-    // the rotation also leaves the column maxima of Z for the heavy build's column scales
-    HIPCHK(hipMemsetAsync(c->d_csmax.p, 0, KP * sizeof(unsigned), st));
-    unsigned* cm = c->d_csmax.as<unsigned>();
-    if (multi) HIPCHK(launch_rotate(KP, S.d_Xfull.as<float>(), c->d_P.as<float>(), S.d_Z.as<float>(), S.prows(), st, cm));
-    else HIPCHK(launch_rotate(KP, S.d_X.as<float>(), c->d_P.as<float>(), S.d_Z.as<float>(), S.own_n, st, cm));
-    have_cmax = true;
+    // world > 1: every rank rotates the whole gathered src (no collective on the critical path)
+    const float* Xs = multi ? S.d_Xfull.as<float>() : S.d_X.as<float>();
+    const int64_t ns = multi ? S.prows() : S.own_n;
+    if (rotate_bf_on(c)) {
+      // bf16 MFMA rotation with the heavy build's split in the same pass.  Its column scales come
+      // first, from a bound: Σ_i Z_ij² = p_jᵀ G p_j, which is λ_j up to the fp32 rounding of P and of
+      // the product (≤ 1e-6 λ_max), so max_i |Z_ij| ≤ √(λ_j + 1e-6 λ_max).  The split's fp16 range
+      // needs the scaled maxima below 2^16; the scales put the bound at 2^13 (colscale_kernel).
+      std::vector<float>& ub = c->h_ub;
+      ub.assign(KP, 0.f);
+      for (int j = 0; j < k; ++j) ub[j] = (float)(std::sqrt(std::max(w[j], 0.0) + 1e-6 * std::max(wmax, 0.0)) * 1.001);
+      HIPCHK(hipMemcpyAsync(c->d_csmax.p, ub.data(), KP * 4, hipMemcpyHostToDevice, st));
+      TRYC(column_scales(c, S, T, true));
+      cs_done = true;
+      float sw = 1.f;
+      split_done = presplit_wanted(c, T, &sw);
+      if (split_done) HIPCHK(c->d_Zhl.ensure((size_t)(S.prows() + 1) * KP * 4));
+      HIPCHK(c->d_Pf.ensure((size_t)rotate_bf_pfrag_bytes(KP)));
+      HIPCHK(launch_rotate_bf(KP, Xs, c->d_P.as<float>(), c->d_Pf.p, S.d_Z.as<float>(), ns, c->d_cs.as<float>(), sw,
+                              split_done ? c->d_Zhl.p : nullptr, S.prows(), c->n_cu, st));
+    } else {
+      // the rotation also leaves the column maxima of Z for the heavy build's column scales
+      HIPCHK(hipMemsetAsync(c->d_csmax.p, 0, KP * sizeof(unsigned), st));
+      HIPCHK(launch_rotate(KP, Xs, c->d_P.as<float>(), S.d_Z.as<float>(), ns, st, c->d_csmax.as<unsigned>()));
+      have_cmax = true;
+    }
   } else {
     HIPCHK(hipEventRecord(ev[1], st));
     HIPCHK(hipMemsetAsync(c->d_lam.p, 0, KP * 4, st));
@@ -904,10 +945,10 @@ int half_sweep(als_ctx* c, int t) {
     else HIPCHK(hipMemcpyAsync(S.d_Z.p, S.d_X.p, (size_t)S.own_n * KP * 4, hipMemcpyDeviceToDevice, st));
   }
   HIPCHK(hipEventRecord(ev[3], st));
-  TRYC(column_scales(c, S, T, have_cmax));
+  if (!cs_done) TRYC(column_scales(c, S, T, have_cmax));
   const void* zhl = nullptr;
   float wsc = 1.f, inv_sw = 1.f;
-  TRYC(presplit(c, S, T, &zhl, &wsc, &inv_sw));
+  TRYC(presplit(c, S, T, &zhl, &wsc, &inv_sw, split_done));
   HIPCHK(hipEventRecord(ev[4], st));
   HIPCHK(hipMemsetAsync(c->d_err.p, 0, 4, st));
   SolveArgs a{};

@@ -149,6 +149,166 @@ __global__ void gram_reduce_kernel(const double* __restrict__ slab, int nblk, do
   G[c2 * KP + c1] = s;
 }
 
+// ---- Gram on bf16 MFMA (KP = 128) -----------------------------------------------------------
+// Each fp32 x = h + m + l (three bf16 parts, exact to 2^-24), products hh, hm, mh, hl, lh, mm on
+// v_mfma_f32_16x16x32_bf16 (32 rows per instruction) instead of fp32 16x16x4 (4 rows): the fp32
+// form ran the Gram MFMA-bound (55 % busy, r03 c4 counters).  The block stages 32 rows at a time in
+// LDS as three bf16 planes (row r: plane p at bytes 256p.., 16-B chunks xor-swizzled by gram_pre_f(r)
+// so the transposed reads below are conflict-free), and every wave reads the MFMA operands of the
+// 8 column blocks with ds_read_b64_tr_b16: lane i + 16q gets column 16A + i of rows 8q .. 8q+7.
+// Wave w owns the upper tiles (a, b) with a ∈ {w, 7 - w} (9 tiles each); fp32 partials go to fp64
+// every 64 rows, like gram_body.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4 mfma_b(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int gram_pre_f(int r) { return 2 * ((r & 3) | ((r & 8) >> 1)); }
+typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+typedef short i16x4_vs __attribute__((__vector_size__(8)));
+__device__ __forceinline__ bf16x4v gram_tr_read(const char* p) {
+  const i16x4_vs v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4_vs*)(p));
+  return __builtin_bit_cast(bf16x4v, v);
+}
+constexpr int GBF_RB = 768;  // LDS bytes per staged row: three 256-B bf16 planes
+
+template <int W>
+__device__ __forceinline__ void gram_bf_body(const float* __restrict__ X, int64_t rb, int64_t re, double* __restrict__ out,
+                                             char* st) {
+  constexpr int KP = 128, NQ = 8, A0 = W, A1 = NQ - 1 - W, NTW = 9;
+  const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, q = lane >> 4;
+  f32x4 acc[NTW];
+  double acc64[NTW][4];
+#pragma unroll
+  for (int s = 0; s < NTW; ++s) {
+    acc[s] = zero4();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc64[s][r] = 0.0;
+  }
+  // staging map: thread t holds float4 (row (t + 256m) >> 5, column 4((t + 256m) & 31)), m = 0..3
+  auto xload = [&](int64_t r0, f32x4 (&xv)[4]) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int idx = tid + 256 * m;
+      const int64_t row = r0 + (idx >> 5);
+      xv[m] = row < re ? ld4(X + row * KP + 4 * (idx & 31)) : zero4();
+    }
+  };
+  f32x4 xn[4];
+  if (rb < re) xload(rb, xn);
+  int chunk = 0;
+  for (int64_t r0 = rb; r0 < re; r0 += 32, ++chunk) {
+    // stage: split into three bf16 planes
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int idx = tid + 256 * m, r = idx >> 5, c = 4 * (idx & 31);
+      bf16x4v ph, pm, pl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = xn[m][e];
+        const __bf16 h = (__bf16)v;
+        const float r1 = v - (float)h;
+        const __bf16 mm = (__bf16)r1;
+        ph[e] = h;
+        pm[e] = mm;
+        pl[e] = (__bf16)(r1 - (float)mm);
+      }
+      char* rowp = st + r * GBF_RB + 2 * (c & 7) + 16 * ((c >> 3) ^ gram_pre_f(r));
+      *reinterpret_cast<bf16x4v*>(rowp) = ph;
+      *reinterpret_cast<bf16x4v*>(rowp + 256) = pm;
+      *reinterpret_cast<bf16x4v*>(rowp + 512) = pl;
+    }
+    __syncthreads();
+    if (r0 + 32 < re) xload(r0 + 32, xn);  // the next chunk's rows in flight over the MFMAs
+    // operands of the column blocks this wave touches (A >= W): lane i + 16q = column 16A + i of
+    // rows 8q .. 8q+7, per plane
+    bf16x8 fr[NQ][3];
+    {
+      const int qq = i16 >> 2, p = i16 & 3;
+      static_for<W, NQ>([&](auto AA) {
+        constexpr int A = decltype(AA)::value;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int r = 8 * q + 4 * h + qq;
+          const char* row = st + r * GBF_RB + 8 * (p & 1) + 16 * ((2 * A + (p >> 1)) ^ gram_pre_f(r));
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) {
+            const bf16x4v v = gram_tr_read(row + 256 * pl);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) fr[A][pl][4 * h + e] = v[e];
+          }
+        }
+      });
+    }
+    __syncthreads();  // the stage is free for the next chunk
+    auto tile = [&](auto SS, auto AA, auto BB) {
+      constexpr int s = decltype(SS)::value, a = decltype(AA)::value, b = decltype(BB)::value;
+      f32x4 c = acc[s];
+      c = mfma_b(fr[a][2], fr[b][0], c);  // the small terms first
+      c = mfma_b(fr[a][0], fr[b][2], c);
+      c = mfma_b(fr[a][1], fr[b][1], c);
+      c = mfma_b(fr[a][1], fr[b][0], c);
+      c = mfma_b(fr[a][0], fr[b][1], c);
+      c = mfma_b(fr[a][0], fr[b][0], c);
+      acc[s] = c;
+    };
+    static_for<0, NQ - A0>([&](auto BB) {
+      tile(BB, std::integral_constant<int, A0>{}, std::integral_constant<int, A0 + decltype(BB)::value>{});
+    });
+    static_for<0, NQ - A1>([&](auto BB) {
+      tile(std::integral_constant<int, NQ - A0 + decltype(BB)::value>{}, std::integral_constant<int, A1>{},
+           std::integral_constant<int, A1 + decltype(BB)::value>{});
+    });
+    if (chunk & 1) {  // 64 rows per fp32 partial, then fp64
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc64[t][r] += (double)acc[t][r];
+        acc[t] = zero4();
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NTW; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc64[t][r] += (double)acc[t][r];
+  // slab: tile (a, b) at its upper_tile index, lane-major like gram_body (natural column blocks)
+#pragma unroll
+  for (int s = 0; s < NTW; ++s) {
+    const int a = s < NQ - A0 ? A0 : A1;
+    const int b = s < NQ - A0 ? A0 + s : A1 + (s - (NQ - A0));
+    const int t = a * NQ - a * (a - 1) / 2 + (b - a);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[((size_t)t * 64 + lane) * 4 + r] = acc64[s][r];
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void gram_bf_kernel(const float* __restrict__ X, int64_t n, int64_t per_blk,
+                                                        double* __restrict__ slab) {
+  constexpr int NT = 36;
+  __shared__ __attribute__((aligned(16))) char st[32 * GBF_RB];
+  const int64_t rb = (int64_t)blockIdx.x * per_blk;
+  const int64_t re = rb + per_blk < n ? rb + per_blk : n;
+  double* out = slab + (size_t)blockIdx.x * NT * 256;
+  const int wave = threadIdx.x >> 6;
+  static_for<0, 4>([&](auto w) {
+    if (wave == decltype(w)::value) gram_bf_body<decltype(w)::value>(X, rb, re, out, st);
+  });
+}
+
+// natural column blocks (gram_bf_kernel): tile t = (a, b), lane l, r -> G[16a + 4(l >> 4) + r][16b + (l & 15)]
+__global__ void gram_reduce_nat_kernel(const double* __restrict__ slab, int nblk, double* __restrict__ G, int KP) {
+  const int NQ = KP / 16, NT = NQ * (NQ + 1) / 2;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= NT * 256) return;
+  double s = 0.0;
+  for (int b = 0; b < nblk; ++b) s += slab[(size_t)b * NT * 256 + e];
+  const int t = e >> 8, lane = (e >> 2) & 63, r = e & 3;
+  const TilePair p = upper_tile(t, NQ);
+  const int c1 = 16 * p.a + 4 * (lane >> 4) + r, c2 = 16 * p.b + (lane & 15);
+  G[c1 * KP + c2] = s;
+  G[c2 * KP + c1] = s;
+}
+
 int gram_slab_blocks(int KP, int64_t n) {
   (void)KP;
   int64_t b = (n + 255) / 256;
@@ -169,8 +329,15 @@ hipError_t launch_gram(int KP, const float* X, int64_t n, double* slab, int nblk
     gram_partial_kernel<64><<<nblk, 256, 0, s>>>(X, n, per, slab);
     gram_reduce_kernel<64><<<(nt * 256 + 255) / 256, 256, 0, s>>>(slab, nblk, G);
   } else if (KP == 128) {
-    gram_partial_kernel<128><<<nblk, 256, 0, s>>>(X, n, per, slab);
-    gram_reduce_kernel<128><<<(nt * 256 + 255) / 256, 256, 0, s>>>(slab, nblk, G);
+    // bf16 MFMA form unless ALBEDO_GRAM_BF=0 (the fp32 16x16x4 form, A/B)
+    static const bool bf = !(getenv("ALBEDO_GRAM_BF") && atoi(getenv("ALBEDO_GRAM_BF")) == 0);
+    if (bf) {
+      gram_bf_kernel<<<nblk, 256, 0, s>>>(X, n, (per + 63) & ~int64_t(63), slab);
+      gram_reduce_nat_kernel<<<(nt * 256 + 255) / 256, 256, 0, s>>>(slab, nblk, G, 128);
+    } else {
+      gram_partial_kernel<128><<<nblk, 256, 0, s>>>(X, n, per, slab);
+      gram_reduce_kernel<128><<<(nt * 256 + 255) / 256, 256, 0, s>>>(slab, nblk, G);
+    }
   } else if (KP == 256) {
     gram_partial_kernel<256><<<dim3(nblk, gram_waves<256>() / 4), 256, 0, s>>>(X, n, per, slab);
     gram_reduce_kernel<256><<<(nt * 256 + 255) / 256, 256, 0, s>>>(slab, nblk, G);
@@ -258,6 +425,153 @@ __global__ __launch_bounds__(64 * ROT_WAVES) void rotate_kernel(const float* __r
     }
   }
 }
+
+// ---- Rotation on bf16 MFMA (KP = 128) -------------------------------------------------------
+// Z = X·P with both operands split into three bf16 parts (x = h + m + l exactly to 2^-24: 8 + 8 + 8
+// significant bits, fp32's exponent range, so no scaling) and the six products above 2^-24
+// (hh, hm, mh, hl, lh, mm) on v_mfma_f32_16x16x32_bf16: 6 x 16 cycles per 32-deep k-step against
+// 8 x 32 for the fp32 16x16x4 form, so the rotation leaves the MFMA bound (74 % busy, r03 c4
+// counters) for the HBM one.  One wave per 16 src rows: lane i + 16q loads X[r0 + i][32kc + 8q ..
+// +7] (the A operand straight from HBM, 4 lanes per 128-B row segment), P's parts sit in LDS in
+// B-fragment order.  With Zhl set the heavy build's operand split is written in the same pass
+// (v = z·(sw·cs), hi = fp16(v), lo = fp16(v - hi): presplit_kernel's arithmetic), so Z is not read
+// back; cs then comes from a bound on the column maxima known before the rotation (engine).
+// P's parts in B-fragment order: element ((J·NK + kc)·3 + part)·512 + l·8 + h holds part `part` of
+// P[32 kc + 8 (l >> 4) + h][16 J + (l & 15)]
+__global__ void rotate_pfrag_kernel(const float* __restrict__ P, __bf16* __restrict__ Pf, int KP) {
+  const int NK = KP / 32;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;  // (J, kc, l, h)
+  if (e >= KP * KP) return;
+  const int h = e & 7, l = (e >> 3) & 63, kc = (e >> 9) % NK, J = (e >> 9) / NK;
+  const float v = P[(32 * kc + 8 * (l >> 4) + h) * KP + 16 * J + (l & 15)];
+  const __bf16 ph = (__bf16)v;
+  const float r1 = v - (float)ph;
+  const __bf16 pm = (__bf16)r1;
+  const __bf16 pl = (__bf16)(r1 - (float)pm);
+  const int base = ((J * NK + kc) * 3) * 512 + l * 8 + h;
+  Pf[base] = ph;
+  Pf[base + 512] = pm;
+  Pf[base + 1024] = pl;
+}
+
+constexpr int RBF_WAVES = 8, RBF_TS = 20;  // waves per block, transpose row stride (floats)
+template <int KP>
+__global__ __launch_bounds__(64 * RBF_WAVES) void rotate_bf_kernel(const float* __restrict__ X, const __bf16* __restrict__ Pf,
+                                                                  float* __restrict__ Z, int64_t n, const float* __restrict__ cs,
+                                                                  float sw, _Float16* __restrict__ Zhl, int64_t zrow) {
+  constexpr int NK = KP / 32, NJ = KP / 16;
+  extern __shared__ __attribute__((aligned(16))) __bf16 sPf[];
+  for (int e = threadIdx.x; e < KP * KP * 3 / 8; e += 64 * RBF_WAVES)
+    reinterpret_cast<int4*>(sPf)[e] = reinterpret_cast<const int4*>(Pf)[e];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i16 = lane & 15, q = lane >> 4;
+  if (Zhl && blockIdx.x == 0)  // the zero row the heavy build's clamped gathers read
+    for (int c = threadIdx.x; c < 2 * KP; c += 64 * RBF_WAVES) Zhl[zrow * 2 * KP + c] = (_Float16)0.f;
+  if (Zhl)
+    for (int c = threadIdx.x; c < KP; c += 64 * RBF_WAVES)
+      reinterpret_cast<float*>(sPf + KP * KP * 3)[RBF_WAVES * 16 * RBF_TS + c] = sw * cs[c];
+  __syncthreads();
+  const int64_t ntile = (n + 15) / 16;
+  // this wave's output transpose (C layout -> rows of 4 consecutive columns per lane), 20-float rows;
+  // then sw·cs per column (a global load in the loop would make its vmcnt wait cover the prefetch)
+  float* tsc = reinterpret_cast<float*>(sPf + KP * KP * 3) + wave * 16 * RBF_TS;
+  float* scs = reinterpret_cast<float*>(sPf + KP * KP * 3) + RBF_WAVES * 16 * RBF_TS;
+  // the next tile's X rows are loaded while this one is on MFMA
+  auto xload = [&](int64_t t, f32x4 (&xv)[NK][2]) {
+    const int64_t row = 16 * t + i16;
+    const float* src = X + (row < n ? row : n - 1) * KP + 8 * q;  // unconditional, zeroed past n
+#pragma unroll
+    for (int kc = 0; kc < NK; ++kc) {
+      xv[kc][0] = ld4(src + 32 * kc);
+      xv[kc][1] = ld4(src + 32 * kc + 4);
+    }
+  };
+  const int64_t tstep = (int64_t)gridDim.x * RBF_WAVES;
+  int64_t t = (int64_t)blockIdx.x * RBF_WAVES + wave;
+  f32x4 xn[NK][2];
+  if (t < ntile) xload(t, xn);
+  for (; t < ntile; t += tstep) {
+    const int64_t r0 = 16 * t;
+    // A operand: row r0 + i16, columns 32kc + 8q .. +7, split into three bf16 parts
+    bf16x8 ah[NK], am[NK], al[NK];
+    {
+      const bool in = r0 + i16 < n;
+#pragma unroll
+      for (int kc = 0; kc < NK; ++kc)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = in ? xn[kc][e >> 2][e & 3] : 0.f;
+          const __bf16 h = (__bf16)v;
+          const float r1 = v - (float)h;
+          const __bf16 m = (__bf16)r1;
+          ah[kc][e] = h;
+          am[kc][e] = m;
+          al[kc][e] = (__bf16)(r1 - (float)m);
+        }
+    }
+    if (t + tstep < ntile) xload(t + tstep, xn);
+    // output rows: lane l writes row r0 + (l >> 2), columns 16J + 4(l & 3) .. +3
+    const int orow = lane >> 2, oc = 4 * (lane & 3);
+    const int64_t rr = r0 + orow;
+#pragma unroll 2
+    for (int J = 0; J < NJ; ++J) {
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int kc = 0; kc < NK; ++kc) {
+        const __bf16* pf = sPf + ((J * NK + kc) * 3) * 512 + lane * 8;
+        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(pf);
+        const bf16x8 bm = *reinterpret_cast<const bf16x8*>(pf + 512);
+        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(pf + 1024);
+        acc = mfma_b(al[kc], bh, acc);  // the small terms first
+        acc = mfma_b(ah[kc], bl, acc);
+        acc = mfma_b(am[kc], bm, acc);
+        acc = mfma_b(am[kc], bh, acc);
+        acc = mfma_b(ah[kc], bm, acc);
+        acc = mfma_b(ah[kc], bh, acc);
+      }
+      // C layout (lane j + 16q: Z[r0 + 4q + r][16J + j]) -> LDS -> 16-B row pieces
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tsc[(4 * q + r) * RBF_TS + i16] = acc[r];
+      WAVE_LDS_SYNC();
+      const f32x4 z4 = ld4(tsc + orow * RBF_TS + oc);
+      WAVE_LDS_SYNC();
+      const int c = 16 * J + oc;
+      if (rr < n) {
+        *reinterpret_cast<f32x4*>(Z + rr * KP + c) = z4;
+        if (Zhl) {
+          f16x4 h4, l4;
+          const f32x4 cw4 = ld4(scs + c);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float v = z4[e] * cw4[e];
+            asm("" : "+v"(v));  // one fp32 rounding; hi and lo both from that value (presplit_kernel)
+            const _Float16 hv = (_Float16)v;
+            h4[e] = hv;
+            l4[e] = (_Float16)(v - (float)hv);
+          }
+          *reinterpret_cast<f16x4*>(Zhl + rr * 2 * KP + c) = h4;
+          *reinterpret_cast<f16x4*>(Zhl + rr * 2 * KP + KP + c) = l4;
+        }
+      }
+    }
+  }
+}
+
+hipError_t launch_rotate_bf(int KP, const float* X, const float* P, void* Pf, float* Z, int64_t n, const float* cs, float sw,
+                            void* Zhl, int64_t zrow, int n_cu, hipStream_t s) {
+  if (KP != 128) return hipErrorInvalidValue;
+  rotate_pfrag_kernel<<<(KP * KP + 255) / 256, 256, 0, s>>>(P, reinterpret_cast<__bf16*>(Pf), KP);
+  if (n <= 0) return hipGetLastError();
+  const size_t lds = (size_t)KP * KP * 3 * 2 + (size_t)RBF_WAVES * 16 * RBF_TS * 4 + (size_t)KP * 4;
+  static const hipError_t attr = allow_lds(rotate_bf_kernel<128>, lds);
+  if (attr != hipSuccess) return attr;
+  const int64_t tiles = (n + 15) / 16;
+  int64_t blocks = (tiles + RBF_WAVES - 1) / RBF_WAVES;
+  if (blocks > n_cu) blocks = n_cu;  // one 96-KiB block per CU, grid-stride over the row tiles
+  rotate_bf_kernel<128><<<(int)blocks, 64 * RBF_WAVES, lds, s>>>(X, reinterpret_cast<const __bf16*>(Pf), Z, n, cs, sw,
+                                                                 reinterpret_cast<_Float16*>(Zhl), zrow);
+  return hipGetLastError();
+}
+int rotate_bf_pfrag_bytes(int KP) { return KP * KP * 3 * 2; }
 
 hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64_t n, hipStream_t s, unsigned* cmax) {
   if (n <= 0) return hipSuccess;

@@ -95,6 +95,12 @@ hipError_t launch_colscale(int KP, const float* Z, int64_t n, float cmax, unsign
 // Zhl[r] = fp16 hi and lo of Z[r][c]·(sw·colscale[c]) (the heavy build's operand split, done once per
 // src row instead of once per gathered rating); row n (the zero row) is cleared
 hipError_t launch_presplit(int KP, const float* Z, int64_t n, const float* colscale, float sw, void* Zhl, hipStream_t s);
+// Z = X·P on bf16 MFMA (three-part split of both operands, KP = 128 only); Pf: rotate_bf_pfrag_bytes
+// of scratch for P's parts; Zhl (or null): the heavy build's operand split written in the same pass
+// (colscale cs and √c sw as launch_presplit, which it replaces), row zrow of Zhl zeroed
+hipError_t launch_rotate_bf(int KP, const float* X, const float* P, void* Pf, float* Z, int64_t n, const float* cs, float sw,
+                            void* Zhl, int64_t zrow, int n_cu, hipStream_t s);
+int rotate_bf_pfrag_bytes(int KP);
 // *out = bits of max |v[i]| (non-negative float, compared as unsigned)
 hipError_t launch_absmax(const float* v, int64_t n, unsigned* out, hipStream_t s);
 // *out = bits of min |v[i]| (0x7f800000 when n = 0)

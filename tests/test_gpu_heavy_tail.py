@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 
 from oracle import spark_als as O
-from tests.test_gpu_parity import Ctx, _rel
+from tests.test_gpu_parity import Ctx, _rel, _row_rel
 
 pytestmark = pytest.mark.gpu
 
@@ -207,3 +207,28 @@ def test_albedo_protocol_at_c1_hyperparameters(gpu_lib, tmp_path):
     assert np.array_equal(gid, rid)
     assert np.array_equal(gsc.view(np.uint32), rsc.astype(np.float32).view(np.uint32))
     _record("albedo_protocol_c1", {"ndcg_gpu": ndcg, "ndcg_oracle": ref, "rel_u": eu, "rel_v": ev})
+
+
+@pytest.mark.parametrize("k", [100, 128])
+def test_gram_padded_rank_128(gpu_lib, k):
+    """Padded rank 128: the Gram runs on bf16 MFMA (each fp32 factor split into three bf16 parts,
+    gram_bf_kernel) and the rotation too (rotate_bf_kernel, with the heavy build's fp16 split written
+    in the same pass from bound-based column scales).  YᵀY against fp64 at 1e-6 on factors whose
+    columns span six decades, 1001 src rows (not a multiple of the 64-row fp32 partials), and the
+    half-sweep's rows against the fp64 oracle at 1e-4."""
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(1001, 150, 20000, seed=53 + k))
+    B = O.make_blocks(d["user"], d["item"], d["rating"])
+    rng = np.random.default_rng(k)
+    U0 = (rng.standard_normal((len(B.user_ids), k)) * np.logspace(-3, 3, k)[None, :]).astype(np.float32)
+    c = Ctx(gpu_lib, k)
+    c.ratings(d["user"], d["item"], d["rating"])
+    c.inject(0, B.user_ids, U0)
+    c.inject(1, B.item_ids, np.zeros((len(B.item_ids), k), np.float32))
+    c.half(1)
+    G = np.empty((k, k))
+    c.L.check(gpu_lib.als_get_gram(c.h, 0, c.L.ptr(G, C.c_double)))
+    assert _rel(G, O.gram(U0)) < 1e-6
+    V_ref = O.half_sweep(U0, B.i_ptr, B.i_col, B.i_val, reg=0.5, alpha=40.0)
+    _, V = c.factors(1)
+    assert _row_rel(V, V_ref) < 1e-4
