@@ -193,10 +193,9 @@ __device__ __forceinline__ void gram_bf_body(const float* __restrict__ X, int64_
       xv[m] = row < re ? ld4(X + row * KP + 4 * (idx & 31)) : zero4();
     }
   };
-  f32x4 xn[4];
-  if (rb < re) xload(rb, xn);
-  int chunk = 0;
-  for (int64_t r0 = rb; r0 < re; r0 += 32, ++chunk) {
+  // two 32-row chunks in flight: buffers xa / xb alternate, each reloaded (two chunks ahead) right
+  // after it has been staged
+  auto step = [&](f32x4 (&xn)[4], int64_t r0, bool flush) {
     // stage: split into three bf16 planes
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
@@ -218,7 +217,7 @@ __device__ __forceinline__ void gram_bf_body(const float* __restrict__ X, int64_
       *reinterpret_cast<bf16x4v*>(rowp + 512) = pl;
     }
     __syncthreads();
-    if (r0 + 32 < re) xload(r0 + 32, xn);  // the next chunk's rows in flight over the MFMAs
+    if (r0 + 64 < re) xload(r0 + 64, xn);
     // operands of the column blocks this wave touches (A >= W): lane i + 16q = column 16A + i of
     // rows 8q .. 8q+7, per plane
     bf16x8 fr[NQ][3];
@@ -258,7 +257,7 @@ __device__ __forceinline__ void gram_bf_body(const float* __restrict__ X, int64_
       tile(std::integral_constant<int, NQ - A0 + decltype(BB)::value>{}, std::integral_constant<int, A1>{},
            std::integral_constant<int, A1 + decltype(BB)::value>{});
     });
-    if (chunk & 1) {  // 64 rows per fp32 partial, then fp64
+    if (flush) {  // 64 rows per fp32 partial, then fp64
 #pragma unroll
       for (int t = 0; t < NTW; ++t) {
 #pragma unroll
@@ -266,6 +265,13 @@ __device__ __forceinline__ void gram_bf_body(const float* __restrict__ X, int64_
         acc[t] = zero4();
       }
     }
+  };
+  f32x4 xa[4], xb[4];
+  if (rb < re) xload(rb, xa);
+  if (rb + 32 < re) xload(rb + 32, xb);
+  for (int64_t r0 = rb; r0 < re; r0 += 64) {
+    step(xa, r0, false);
+    if (r0 + 32 < re) step(xb, r0 + 32, true);
   }
 #pragma unroll
   for (int t = 0; t < NTW; ++t)
@@ -475,24 +481,46 @@ __global__ __launch_bounds__(64 * RBF_WAVES) void rotate_bf_kernel(const float* 
   // then sw·cs per column (a global load in the loop would make its vmcnt wait cover the prefetch)
   float* tsc = reinterpret_cast<float*>(sPf + KP * KP * 3) + wave * 16 * RBF_TS;
   float* scs = reinterpret_cast<float*>(sPf + KP * KP * 3) + RBF_WAVES * 16 * RBF_TS;
-  // the next tile's X rows are loaded while this one is on MFMA
+  // The next tile's X rows are loaded while this one is on MFMA.  The loads are issued from asm so
+  // that the compiler does not track them: its own wait for them at the loop head would be
+  // vmcnt(0), which also waits for every store of the tile in between (GFX9 counts stores in
+  // vmcnt).  xwait() waits for exactly the loads, leaving the tile's stores (NST per tile) in flight.
   auto xload = [&](int64_t t, f32x4 (&xv)[NK][2]) {
     const int64_t row = 16 * t + i16;
     const float* src = X + (row < n ? row : n - 1) * KP + 8 * q;  // unconditional, zeroed past n
 #pragma unroll
     for (int kc = 0; kc < NK; ++kc) {
-      xv[kc][0] = ld4(src + 32 * kc);
-      xv[kc][1] = ld4(src + 32 * kc + 4);
+      const float* p = src + 32 * kc;
+      f32x4 v0, v1;
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v0) : "v"(p) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "=v"(v1) : "v"(p) : "memory");
+      xv[kc][0] = v0;
+      xv[kc][1] = v1;
+    }
+  };
+  auto xwait = [&](f32x4 (&xv)[NK][2], bool after_stores) {
+    if (after_stores && Zhl) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // 3 stores per J
+    else if (after_stores) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // 1 store per J
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int kc = 0; kc < NK; ++kc) {  // the registers are read only after the wait
+      f32x4 v0 = xv[kc][0], v1 = xv[kc][1];
+      asm volatile("" : "+v"(v0), "+v"(v1));
+      xv[kc][0] = v0;
+      xv[kc][1] = v1;
     }
   };
   const int64_t tstep = (int64_t)gridDim.x * RBF_WAVES;
   int64_t t = (int64_t)blockIdx.x * RBF_WAVES + wave;
   f32x4 xn[NK][2];
   if (t < ntile) xload(t, xn);
+  bool after_stores = false;
   for (; t < ntile; t += tstep) {
     const int64_t r0 = 16 * t;
     // A operand: row r0 + i16, columns 32kc + 8q .. +7, split into three bf16 parts
     bf16x8 ah[NK], am[NK], al[NK];
+    xwait(xn, after_stores && r0 - 16 * tstep + 15 < n);  // (a ragged last tile stores fewer)
+    after_stores = true;
     {
       const bool in = r0 + i16 < n;
 #pragma unroll
