@@ -311,6 +311,9 @@ __global__ void gram_reduce_nat_kernel(const double* __restrict__ slab, int nblk
   const int t = e >> 8, lane = (e >> 2) & 63, r = e & 3;
   const TilePair p = upper_tile(t, NQ);
   const int c1 = 16 * p.a + 4 * (lane >> 4) + r, c2 = 16 * p.b + (lane & 15);
+  // a diagonal tile holds (i, j) and (j, i) separately: the split products reach them in different
+  // accumulation orders, so they can differ in the last bit; (i <= j) writes both (deterministic)
+  if (c1 > c2) return;
   G[c1 * KP + c2] = s;
   G[c2 * KP + c1] = s;
 }

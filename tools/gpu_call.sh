@@ -33,6 +33,7 @@ for s in "$@"; do
     nnlstime) timeout -k 5 60 tools/probe/nnlstime 256 100000 2048 200 > gpurun_out/nnlstime.txt 2>&1 ;;
     ab_rot) for v in 0 1; do ALBEDO_ROTATE_BF=$v timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu --topk-users 0 > gpurun_out/ab_rot_$v.json 2> gpurun_out/ab_rot_$v.err || exit 1; done ;;
     tests_gram) timeout -k 10 300 $PYT tests/test_gpu_heavy_tail.py -k "gram" > gpurun_out/tests_gram.log 2>&1 ;;
+    grid) bash tools/grid_check.sh ;;
     tests_mr) timeout -k 10 900 $PYT tests/test_multi_rank.py > gpurun_out/tests_mr.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
