@@ -34,6 +34,7 @@ for s in "$@"; do
     ab_rot) for v in 0 1; do ALBEDO_ROTATE_BF=$v timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu --topk-users 0 > gpurun_out/ab_rot_$v.json 2> gpurun_out/ab_rot_$v.err || exit 1; done ;;
     tests_gram) timeout -k 10 300 $PYT tests/test_gpu_heavy_tail.py -k "gram" > gpurun_out/tests_gram.log 2>&1 ;;
     grid) bash tools/grid_check.sh ;;
+    trace_c5) mkdir -p gpurun_out/trace_c5 && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_c5 -o run -- python3 -u bench.py --config c5 --steps 1 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/trace_c5/bench.json 2> gpurun_out/trace_c5/bench.err ;;
     tests_mr) timeout -k 10 900 $PYT tests/test_multi_rank.py > gpurun_out/tests_mr.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
