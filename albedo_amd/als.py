@@ -164,7 +164,7 @@ class ALS(_Params):
                                            "No ratings available from the input dataset.")
         return np.ascontiguousarray(user), np.ascontiguousarray(item), rating
 
-    def fit(self, dataset, params=None, initialUserFactors=None, initialItemFactors=None):
+    def fit(self, dataset, params=None, initialUserFactors=None, initialItemFactors=None, parallelism=8):
         """ALS.fit (Spark Estimator.fit(dataset[, paramMap | paramMaps])).
 
         `params` = one ParamMap (dict) -> one ALSModel fitted with those overrides; a list of ParamMaps
@@ -172,9 +172,10 @@ class ALS(_Params):
         (id remap, both CSR orientations, shards) on the device: between fits only the
         rank-dependent buffers are rebuilt (als_set_params).  The column names must agree across the
         maps.  `initial*Factors` = (ids, factors[n, rank]) injects the start point (parity path, one
-        map only); without it the Spark-style XORShiftRandom initialisation is used."""
+        map only); without it the Spark-style XORShiftRandom initialisation is used.  `parallelism`
+        (the name of Spark 2.3's CrossValidator knob) caps the maps of a list fitted at once."""
         if isinstance(params, (list, tuple)):
-            return self._fit_many(dataset, [self._param_map(pm) for pm in params])
+            return self._fit_many(dataset, [self._param_map(pm) for pm in params], max_concurrent=parallelism)
         pm = self._param_map(params or {})
         user, item, rating = self._ratings(dataset, pm)
         lib = load()
@@ -200,7 +201,12 @@ class ALS(_Params):
     def _fit_many(self, dataset, maps, max_concurrent=8):
         """The CV grid (ALSRecommenderCV.scala:67-90): one ingest; the maps of one rank are fitted
         CONCURRENTLY, each on an als_fork of the ingest context (own factors and streams, shared CSR)
-        driven by its own host thread; every model is bit-identical to its standalone fit."""
+        driven by its own host thread; every model is bit-identical to its standalone fit.
+
+        Each fork holds its own factor, rotation and split-K buffers, so at most `max_concurrent`
+        forks exist at once and fewer when the device runs out of memory: a fork or a fit that fails
+        with ALS_E_OUT_OF_MEMORY ends the batch, and its map runs again in a smaller batch (alone, if
+        need be: the sequential path)."""
         if not maps:
             return []
         from concurrent.futures import ThreadPoolExecutor
@@ -212,35 +218,57 @@ class ALS(_Params):
         lib = load()
         h = self._context(maps[0])
         models = [None] * len(maps)
+
+        def run(fh):
+            t0 = time.perf_counter()
+            check(lib.als_fit(fh))
+            return time.perf_counter() - t0
+
+        def oom(e):
+            return isinstance(e, _lib.ALSError) and e.code == _lib.ALS_E_OUT_OF_MEMORY
+
         try:
             for pm in maps:  # validate every map before the ingest (no fit runs on a bad grid)
                 check(lib.als_set_params(h, C.byref(self._c_params(pm))))
             check(lib.als_set_ratings(h, user.size, ptr(user, C.c_int32), ptr(item, C.c_int32),
                                       ptr(rating, C.c_float)))
             groups = {}
-            for i, pm in enumerate(maps):  # forks share the layout of one (rank, nonnegative)
-                groups.setdefault((int(pm["rank"]), bool(pm["nonnegative"])), []).append(i)
+            for i, pm in enumerate(maps):  # forks share the layout of one (rank, nonnegative, light limit)
+                key = (int(pm["rank"]), bool(pm["nonnegative"]), int(pm["lightMaxDegree"]))
+                groups.setdefault(key, []).append(i)
             for idx in groups.values():
                 check(lib.als_set_params(h, C.byref(self._c_params(maps[idx[0]]))))
-                forks = []
-                try:
-                    for i in idx:
-                        fh = C.c_void_p()
-                        check(lib.als_fork(h, C.byref(self._c_params(maps[i])), C.byref(fh)))
-                        forks.append(fh)
-
-                    def run(fh):
-                        t0 = time.perf_counter()
-                        check(lib.als_fit(fh))
-                        return time.perf_counter() - t0
-
-                    with ThreadPoolExecutor(max_workers=max(1, min(max_concurrent, len(forks)))) as ex:
-                        secs = list(ex.map(run, forks))
-                    for i, fh, fit_s in zip(idx, forks, secs):
-                        models[i] = self._snapshot(fh, maps[i], fit_s)
-                finally:
-                    for fh in forks:
-                        lib.als_destroy(fh)
+                todo = list(idx)
+                cap = max(1, int(max_concurrent))
+                while todo:
+                    forks = []
+                    try:
+                        for i in todo[:cap]:
+                            fh = C.c_void_p()
+                            try:
+                                check(lib.als_fork(h, C.byref(self._c_params(maps[i])), C.byref(fh)))
+                            except _lib.ALSError as e:
+                                if not (oom(e) and forks):
+                                    raise
+                                break  # fit the forks that fit in memory first
+                            forks.append((i, fh))
+                        with ThreadPoolExecutor(max_workers=len(forks)) as ex:
+                            futs = [ex.submit(run, fh) for _, fh in forks]
+                        done, failed = [], []
+                        for (i, fh), fu in zip(forks, futs):
+                            e = fu.exception()
+                            if e is None:
+                                models[i] = self._snapshot(fh, maps[i], fu.result())
+                                done.append(i)
+                            elif oom(e) and len(forks) > 1:
+                                failed.append(i)
+                            else:
+                                raise e
+                        cap = len(forks) if not failed else max(1, len(forks) // 2)
+                        todo = [i for i in todo if i not in done]
+                    finally:
+                        for _, fh in forks:
+                            lib.als_destroy(fh)
         finally:
             lib.als_destroy(h)
         return models

@@ -79,6 +79,7 @@ struct DevBuf {
     owned = false;
   }
   hipError_t ensure(size_t b) {
+    if (!owned) return hipErrorNotSupported;  // a view (als_fork) is never resized or written through
     if (b <= bytes && p) return hipSuccess;
     release();
     hipError_t e = hipMalloc(&p, b ? b : 16);
@@ -498,7 +499,17 @@ int factor_buffers(als_ctx* c) {
 }
 
 // ---- ingest -------------------------------------------------------------------------------------
+// A fork views its parent's ingest, and a parent's ingest is viewed by its live forks: neither may
+// rebuild it (a re-ingest would write through the views or free buffers the forks still read).
+int ingest_allowed(als_ctx* c) {
+  std::lock_guard<std::mutex> lk(g_fork_mu);
+  if (c->parent) return fail(ALS_E_STATE, "new ratings on a fork (set them on a fresh context instead)");
+  if (c->forks > 0) return fail(ALS_E_STATE, "new ratings while forks view this context's ingest");
+  return ALS_OK;
+}
+
 int ingest_device(als_ctx* c, int64_t n, const int32_t* d_user, const int32_t* d_item, const float* d_rating) {
+  TRYC(ingest_allowed(c));
   if (n <= 0)
     return fail(ALS_E_INVALID_ARGUMENT, "No ratings available from the input dataset (empty ratings).");
   TRYC(set_device(c));
@@ -1317,6 +1328,7 @@ int als_set_ratings(als_ctx* c, int64_t n, const int32_t* user, const int32_t* i
   if (!c) return fail(ALS_E_INVALID_ARGUMENT, "null context");
   if (n <= 0) return fail(ALS_E_INVALID_ARGUMENT, "No ratings available from the input dataset (empty ratings).");
   if (!user || !item || !rating) return fail(ALS_E_INVALID_ARGUMENT, "null ratings");
+  TRYC(ingest_allowed(c));
   TRYC(set_device(c));
   DevBuf du, di, dr;
   HIPCHK(du.ensure(n * 4));
@@ -2056,6 +2068,7 @@ int als_set_ratings_synthetic(als_ctx* c, uint64_t seed, int32_t rounds, int64_t
                               const int64_t* deg_prefix, const double* cw, const int32_t* perm) {
   if (!c || !deg_prefix || !cw || !perm || n_users <= 0 || n_items <= 0)
     return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  TRYC(ingest_allowed(c));
   TRYC(set_device(c));
   const int64_t n = deg_prefix[n_users];
   DevBuf dp, dcw, dperm, du, di, dr;

@@ -8,8 +8,9 @@
 //            imposes): one wave per user selects them with a wave bitonic sort.
 //  predicted intoUserPredictedItems (:131-139) of the top-k lists (score desc, id asc): the lists
 //            als_recommend produces, kept on the device.
-//  ndcgAt    per user n = min(max(|pred|, |lab|), k), dcg = Σ_{i<n} [pred_i ∈ lab] g_i,
-//            maxDcg = Σ_{i<min(n,|lab|)} g_i, g_i = 1 / ln(i + 2) from the host's libm (the same
+//  ndcgAt    per user n = min(max(|pred|, |labSet|), k), dcg = Σ_{i<n} [pred_i ∈ lab] g_i,
+//            maxDcg = Σ_{i<min(n,|labSet|)} g_i (|labSet| = distinct items of the actual list),
+//            g_i = 1 / ln(i + 2) from the host's libm (the same
 //            table the host evaluator uses), summed in index order: per-user values are bit-identical
 //            to the host evaluator's.
 #include <hip/hip_runtime.h>
@@ -118,18 +119,24 @@ __global__ __launch_bounds__(256) void ev_ndcg_kernel(const int32_t* __restrict_
   const int32_t p = lane < k ? pred[u * k + lane] : -1;
   const int nl = act_n[u];
   const int32_t lab = lane < nl ? act[u * k + lane] : -1;
-  bool hit = false;
-  for (int j = 0; j < nl; ++j) hit |= (p >= 0 && p == __shfl(lab, j));
+  bool hit = false, dup = false;
+  for (int j = 0; j < nl; ++j) {
+    const int32_t v = __shfl(lab, j);
+    hit |= (p >= 0 && p == v);
+    dup |= (j < lane && v == lab);  // an earlier entry holds the same item
+  }
+  // |labSet|: mllib takes the size of the label SET (a user's duplicated (user, item) rows count once)
+  const int ns = __popcll(__ballot(lane < nl && !dup));
   const int np = __popcll(__ballot(lane < k && p >= 0));  // the lists are dense: -1 only at the tail
   const uint64_t hits = __ballot(hit);
   if (lane == 0) {
     double v = 0.0;
-    if (nl > 0) {
-      const int n = min(max(np, nl), k);
+    if (ns > 0) {
+      const int n = min(max(np, ns), k);
       double dcg = 0.0, mx = 0.0;
       for (int i = 0; i < n; ++i) {
         if (i < np && ((hits >> i) & 1)) dcg += gain[i];
-        if (i < nl) mx += gain[i];
+        if (i < ns) mx += gain[i];
       }
       v = dcg / mx;
     }

@@ -32,6 +32,14 @@
 namespace albedo {
 namespace {
 
+#ifdef WAVE_PROBE_STAMPS  // probes only (tools/probe/wavetime.hip): per-row shader-clock stamps
+__device__ unsigned long long* g_wave_stamps;  // [rows][4]: start, build done, factor done, stored
+#define WAVE_STAMP(row, i) \
+  if ((threadIdx.x & 63) == 0) g_wave_stamps[(row) * 4 + (i)] = __builtin_amdgcn_s_memtime()
+#else
+#define WAVE_STAMP(row, i) (void)0
+#endif
+
 typedef __attribute__((address_space(3))) void* lds_vp;
 typedef __attribute__((address_space(1))) const void* glb_vp;
 
@@ -290,7 +298,9 @@ __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
   const int d = (int)(a.ptr[j + 1] - p0);
   f32x4 acc[NT];
   float bacc[NQ];
+  WAVE_STAMP(ridx, 0);
   const int npos = wave_build<KP, IMPLICIT, PRE>(a, p0, d, st, s_cs, acc, bacc);
+  WAVE_STAMP(ridx, 1);
   const float lamn = a.reg * (float)(IMPLICIT ? npos : d);
   const float* isc = s_cs + KP;
   // The system is scaled by s2 = 4^e (exact) so that its largest diagonal entry stays below 2^28:
@@ -339,6 +349,7 @@ __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
   // ---- blocked Cholesky A' = UᵀU on the tiles, RHS alongside (wave_chol.h) -----------------------
   float xs[NQ];
   const bool notpd = wave_chol_solve<NQ, true>(acc, bacc, reinterpret_cast<float*>(st), xs);
+  WAVE_STAMP(ridx, 2);
   bool nonfinite = false;
 #pragma unroll
   for (int A = 0; A < NQ; ++A) {
@@ -347,6 +358,7 @@ __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
     nonfinite |= !isfinite(v);
     if (q == 0) a.X[(int64_t)j * KP + c] = v;
   }
+  WAVE_STAMP(ridx, 3);
   const bool bad = notpd || __any(nonfinite);  // wave-uniform
   if (lane == 0 && bad) atomicOr(a.err, 2);
 }

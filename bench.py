@@ -178,8 +178,11 @@ def main():
             traffic = float(sum(found))
 
     # ---- top-30 users/s (secondary metric; a bounded user subset) ------------------------------
+    # world > 1: every rank calls als_recommend (the users are sharded across the ranks, each scores
+    # its slice against the replicated dst factors, the lists are all-gathered); timed between
+    # barriers, max over ranks
     topk_ups = topk_info = None
-    if args.topk_users != 0 and world == 1:
+    if args.topk_users != 0:
         ids = np.empty(n_users, np.int32)
         L.check(lib.als_get_ids(h, 0, L.ptr(ids, C.c_int32)))
         every = args.topk_users < 0 or args.topk_users >= n_users
@@ -193,11 +196,18 @@ def main():
                                   L.ptr(out_i, C.c_int32), L.ptr(out_s, C.c_float)))  # warm
         st0 = np.zeros(4, np.int64)
         L.check(lib.als_topk_stats(h, L.ptr(st0, C.c_int64)))
+        barrier()
         t1 = time.perf_counter()
         # every user: recommendForAllUsers (subset = NULL); else ALSModel.recommendForUserSubset
         L.check(lib.als_recommend(h, 0, 30, None if every else L.ptr(sub, C.c_int32), sub.size, None,
                                   L.ptr(out_i, C.c_int32), L.ptr(out_s, C.c_float)))
+        barrier()
         topk_s = time.perf_counter() - t1
+        if dist is not None:
+            import torch
+            t = torch.tensor([topk_s], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            topk_s = float(t.item())
         topk_ups = sub.size / topk_s
         st1 = np.zeros(4, np.int64)
         L.check(lib.als_topk_stats(h, L.ptr(st1, C.c_int64)))

@@ -309,10 +309,35 @@ def test_cv_grid_concurrent_forks(gpu_lib):
     L.check(gpu_lib.als_fork(c.h, C.byref(p), C.byref(f)))
     with pytest.raises(L.IllegalStateException):
         L.check(gpu_lib.als_set_params(c.h, C.byref(p)))
+    # neither the fork (its ingest is a view) nor the forked parent (viewed) may re-ingest
+    u = np.ascontiguousarray(d["user"][:100], np.int32)
+    i = np.ascontiguousarray(d["item"][:100], np.int32)
+    r = np.ones(100, np.float32)
+    for h in (f, c.h):
+        with pytest.raises(L.IllegalStateException, match="fork"):
+            L.check(gpu_lib.als_set_ratings(h, u.size, L.ptr(u, C.c_int32), L.ptr(i, C.c_int32), L.ptr(r, C.c_float)))
     gpu_lib.als_destroy(c.h)  # the parent outlives it: freed with the fork below
     c.h = None
     L.check(gpu_lib.als_fit(f))
     gpu_lib.als_destroy(f)
+
+
+def test_cv_grid_light_limit_and_parallelism(gpu_lib):
+    """A grid that varies lightMaxDegree (each value its own layout on the parent) fitted with one map
+    at a time (parallelism = 1: the sequential path) and with all at once; every model bit-identical
+    to its standalone fit."""
+    from albedo_amd import ALS
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(1200, 250, 16000, seed=45))
+    grid = [dict(rank=20, regParam=g, lightMaxDegree=lm) for lm in (0, 16, -1) for g in (0.1, 0.5)]
+    base = ALS(implicitPrefs=True, seed=42, maxIter=2, alpha=40.0)
+    seq = base.fit(d, grid, parallelism=1)
+    par = base.fit(d, grid)
+    for pm, a, b in zip(grid, seq, par):
+        solo = ALS(**{**dict(implicitPrefs=True, seed=42, maxIter=2, alpha=40.0), **pm}).fit(d)
+        for m in (a, b):
+            assert np.array_equal(m.user_factors_np()[1], solo.user_factors_np()[1]), pm
+            assert np.array_equal(m.item_factors_np()[1], solo.item_factors_np()[1]), pm
 
 
 def test_facade_fit_matches_oracle_and_ndcg(gpu_lib):
@@ -489,32 +514,61 @@ def test_topk_subset_unknown_ids_and_small_catalogue(gpu_lib):
 
 
 @pytest.mark.parametrize("k", [30, 10])
-def test_device_ndcg_matches_host_evaluator(gpu_lib, k):
+def test_device_ndcg_matches_oracle(gpu_lib, k):
     """RankingEvaluator on the device (als_evaluate_ndcg): actual lists = rank() over starred_at desc
-    (engineered timestamp ties, users with fewer and more than k stars), predicted = the top-k lists,
-    ndcgAt per user bit-identical to the host evaluator (RankingEvaluator.scala:83-139), the mean
-    within 1e-12; users unknown to the model are dropped by the join."""
+    (engineered timestamp ties, users with fewer and more than k stars, duplicated (user, item) rows
+    whose label SET is smaller than the list), predicted = the top-k lists; ndcgAt per user
+    bit-identical to the oracle's (oracle/spark_als.py ndcg_at / into_user_items, which restate
+    RankingEvaluator.scala:83-139 and mllib RankingMetrics.ndcgAt), the mean within 1e-12 of
+    O.evaluate_ndcg; users unknown to the model are dropped by the join."""
     from albedo_amd import ALS
-    from albedo_amd import evaluation as E
     from albedo_amd.synthetic import SynthSpec, generate
     d = generate(SynthSpec(2500, 600, 40000, seed=19), with_timestamps=True)
     model = ALS(rank=24, maxIter=3, regParam=0.5, alpha=40.0, implicitPrefs=True).fit(d)
     rng = np.random.default_rng(k)
     ts = d["ts"] // 1_000_000  # coarse: many equal timestamps within a user (rank() ties)
-    users = np.r_[d["user"], np.full(5, 123456789, np.int32)]  # an id the model does not know
-    items = np.r_[d["item"], d["item"][:5]]
-    keys = np.r_[ts, ts[:5]]
+    dup = rng.choice(d["user"].size, 400, replace=False)  # the same (user, item) again, a later star
+    users = np.r_[d["user"], d["user"][dup], np.full(5, 123456789, np.int32)]  # + an unknown id
+    items = np.r_[d["item"], d["item"][dup], d["item"][:5]]
+    keys = np.r_[ts, ts[dup] + 1 + rng.integers(0, 3, dup.size), ts[:5]]
     perm = rng.permutation(users.size)  # any input order
     mean, uids, vals = model.evaluate_ndcg(users[perm], items[perm], keys[perm], k=k, per_user=True)
-    actual = E.into_user_items(users, items, keys, k)
+    actual = O.into_user_items(users, items, keys, k)
+    assert any(len(set(actual[int(u)][:k])) < len(actual[int(u)][:k]) for u in d["user"][dup])
     src, ids, _ = model.recommend_np(k, subset=uids)
     assert np.array_equal(src, uids)
     pred = {int(u): [int(x) for x in ids[r] if x >= 0] for r, u in enumerate(src)}
     assert 123456789 not in set(uids.tolist()) and uids.size == np.unique(d["user"]).size
-    ref = [E.ndcg_at([(pred[int(u)][:k], actual[int(u)][:k])], k) for u in uids]
+    ref = [O.ndcg_at([(pred[int(u)][:k], actual[int(u)][:k])], k) for u in uids]
     assert np.array_equal(vals, np.asarray(ref))
-    host = E.RankingEvaluator(actual, "NDCG@k", k).evaluate(pred)
+    host = O.evaluate_ndcg(pred, actual, k)
     assert abs(mean - host) <= 1e-12 * max(1.0, abs(host))
+
+
+def test_recommend_for_all_items_and_item_subset(gpu_lib):
+    """recommendForAllItems / recommendForItemSubset (Spark ALSModel, side = item): every item's top-k
+    users, ids and F2J score bits against the oracle scorer with the roles swapped; a subset with an
+    unknown item id gets an empty row."""
+    from albedo_amd import ALS
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(3000, 400, 30000, seed=27))
+    model = ALS(rank=20, maxIter=3, regParam=0.5, alpha=40.0, implicitPrefs=True).fit(d)
+    uids, uf = model.user_factors_np()
+    iids, itf = model.item_factors_np()
+    for num in (30, 100):
+        src, ids, sc = model.recommend_np(num, side=1)
+        assert np.array_equal(src, iids)
+        ref_ids, ref_sc = O.recommend_for_all(iids, itf, uids, uf, num)
+        assert np.array_equal(ids, ref_ids)
+        assert np.array_equal(sc.view(np.uint32), ref_sc.view(np.uint32))
+    sub = np.array([iids[5], 2_000_000_000, iids[-1]], np.int64)
+    df = model.recommendForItemSubset({"item": sub}, 10)
+    assert sorted(df["item"].tolist()) == sorted([int(iids[5]), int(iids[-1])])
+    full = model.recommendForAllItems(10)
+    assert len(full) == iids.size
+    row = full[full["item"] == iids[5]]["recommendations"].iloc[0]
+    ref_ids, _ = O.recommend_for_all(iids[5:6], itf[5:6], uids, uf, 10)
+    assert [u for u, _ in row] == ref_ids[0].tolist()
 
 
 def test_transform_bit_exact_and_cold_start(gpu_lib):
