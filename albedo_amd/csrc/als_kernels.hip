@@ -501,10 +501,17 @@ __global__ __launch_bounds__(64 * RBF_WAVES) void rotate_bf_kernel(const float* 
       xv[kc][1] = v1;
     }
   };
+  // The counts are checked on the emitted ISA at build time (tools/check_rotate_isa.py, Makefile):
+  // when the check fails the object is rebuilt with ALBEDO_ROTATE_VMCNT0 (every wait drains).
   auto xwait = [&](f32x4 (&xv)[NK][2], bool after_stores) {
+#ifdef ALBEDO_ROTATE_VMCNT0
+    (void)after_stores;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
     if (after_stores && Zhl) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // 3 stores per J
     else if (after_stores) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // 1 store per J
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 #pragma unroll
     for (int kc = 0; kc < NK; ++kc) {  // the registers are read only after the wait
       f32x4 v0 = xv[kc][0], v1 = xv[kc][1];
