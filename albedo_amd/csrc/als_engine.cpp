@@ -119,9 +119,10 @@ struct Side {
   bool full_valid = false;       // d_Xfull holds the current X (gathered behind the solve on st2)
   int64_t prows() const { return (int64_t)nch * world * chpad; }
   int64_t pos(int r, int64_t i) const { return (i / chpad) * world * chpad + (int64_t)r * chpad + i % chpad; }
-  std::vector<double> B;         // [KP][KP] basis: original = X · Bᵀ
-  std::vector<double> G;         // last Gram of this side (as src), [rank][rank], in basis GB
-  std::vector<double> GB;        // [KP][KP] the side's basis when G was computed (G_orig = GB G GBᵀ)
+  DevBuf d_B;                    // fp64 [KP][KP] orthogonal basis on the device: original = X · Bᵀ
+  DevBuf d_Gk;                   // fp64 [KP][KP] last Gram of this side (as src), in basis d_GB
+  DevBuf d_GB;                   // fp64 [KP][KP] the side's basis when d_Gk was computed (G_orig = GB G GBᵀ)
+  bool has_gram = false;
   bool has_factors = false;
   double t[ALS_T_COUNT] = {0};
   int64_t stats[4] = {0};
@@ -162,6 +163,7 @@ struct als_ctx {
   bool has_ratings = false;
   bool model_only = false;
   DevBuf slab, d_G, d_P, d_lam, d_err, d_Gt, d_cs, d_csmax;
+  DevBuf d_eig;                  // device eigensolver scratch (eig.hip)
   DevBuf d_partial, d_reduced;   // split-K partial / reduced A' records (shared by both sides)
   DevBuf d_Zhl;                  // pre-split src rows of the uniform-confidence heavy build
   DevBuf d_Pf;                   // P's bf16 parts in MFMA fragment order (rotate_bf)
@@ -173,7 +175,6 @@ struct als_ctx {
   int64_t topk_stats[4] = {0, 0, 0, 0};
   std::vector<int32_t> last_rescan;  // src ids the last als_recommend sent to the exact rescan
   int split_len = 0;             // ratings per split-K chunk (0: no split)
-  std::vector<float> h_P32, h_lam32, h_Gt, h_ub;  // host staging of async H2D copies (outlive the sync)
   int slab_blocks = 0;
   hipEvent_t ev[8] = {};
   hipStream_t st2 = nullptr;     // world > 1: factor-chunk gathers behind the solve
@@ -480,8 +481,11 @@ int factor_buffers(als_ctx* c) {
       HIPCHK(hipMemset(S.d_Xfull.p, 0, S.d_Xfull.bytes));
     }
     S.full_valid = false;
-    S.B.assign((size_t)c->KP * c->KP, 0.0);
-    for (int i = 0; i < c->KP; ++i) S.B[(size_t)i * c->KP + i] = 1.0;
+    HIPCHK(S.d_B.ensure((size_t)c->KP * c->KP * 8));
+    HIPCHK(S.d_Gk.ensure((size_t)c->KP * c->KP * 8));
+    HIPCHK(S.d_GB.ensure((size_t)c->KP * c->KP * 8));
+    HIPCHK(launch_identity(S.d_B.as<double>(), c->KP, c->st));
+    S.has_gram = false;
     S.has_factors = false;
     S.orig_valid = false;
     S.full_valid = false;
@@ -491,6 +495,7 @@ int factor_buffers(als_ctx* c) {
   HIPCHK(c->slab.ensure(gram_slab_doubles(c->KP, c->slab_blocks) * 8));
   HIPCHK(c->d_G.ensure((size_t)c->KP * c->KP * 8));
   HIPCHK(c->d_P.ensure((size_t)c->KP * c->KP * 4));
+  HIPCHK(c->d_eig.ensure(eig_scratch_doubles(c->KP) * 8));
   HIPCHK(c->d_lam.ensure((size_t)c->KP * 4));
   HIPCHK(c->d_err.ensure(16));
   HIPCHK(c->d_cs.ensure((size_t)2 * c->KP * 4));
@@ -606,8 +611,7 @@ int upload_factors(als_ctx* c, int side, const float* f, int64_t ld) {
   for (int64_t r = 0; r < S.own_n; ++r)
     std::memcpy(&h[(size_t)r * c->KP], f + (size_t)(S.own0 + r) * ld, sizeof(float) * c->p.rank);
   HIPCHK(hipMemcpy(S.d_X.p, h.data(), (size_t)S.own_n * c->KP * 4, hipMemcpyHostToDevice));
-  S.B.assign((size_t)c->KP * c->KP, 0.0);
-  for (int i = 0; i < c->KP; ++i) S.B[(size_t)i * c->KP + i] = 1.0;
+  HIPCHK(launch_identity(S.d_B.as<double>(), c->KP, c->st));
   S.has_factors = true;
   S.orig_valid = false;
   S.full_valid = false;
@@ -713,11 +717,10 @@ int half_sweep_nnls(als_ctx* c, int t) {
     TRYC(allreduce_G(c));
     std::vector<double> Gf((size_t)KP * KP);
     HIPCHK(hipMemcpyAsync(Gf.data(), c->d_G.p, Gf.size() * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(S.d_Gk.p, c->d_G.p, (size_t)KP * KP * 8, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.d_GB.p, S.d_B.p, (size_t)KP * KP * 8, hipMemcpyDeviceToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
-    S.G.assign((size_t)k * k, 0.0);
-    for (int i = 0; i < k; ++i)
-      for (int j = 0; j < k; ++j) S.G[(size_t)i * k + j] = Gf[(size_t)i * KP + j];
-    S.GB = S.B;
+    S.has_gram = true;
     for (int i = 0; i < KP; ++i)
       for (int j = 0; j < 16 * ((i >> 4) + 1); ++j) gt[nnls_gtile_index(i, j)] = (float)Gf[(size_t)i * KP + j];
     double gmax = 0.0;
@@ -799,7 +802,7 @@ int half_sweep_nnls(als_ctx* c, int t) {
   T.t[ALS_T_HALF_TOTAL] = event_ms(ev[0], ev[6]);
   if (err & 4) return fail(ALS_E_STATE, "lockstep NNLS row above its degree limit (row layout out of date)");
   if (err) return fail(ALS_E_NOT_POSITIVE_DEFINITE, "NNLS solve produced a non-finite result");
-  T.B = S.B;
+  HIPCHK(hipMemcpyAsync(T.d_B.p, S.d_B.p, (size_t)KP * KP * 8, hipMemcpyDeviceToDevice, st));  // no rotation
   T.has_factors = true;
   T.orig_valid = false;
   T.full_valid = false;
@@ -857,7 +860,6 @@ int half_sweep(als_ctx* c, int t) {
   hipStream_t st = c->st;
   hipEvent_t* ev = c->ev;
   const bool multi = c->world > 1;
-  double eig_ms = 0.0;
   bool have_cmax = false, cs_done = false, split_done = false;
   bool force_heavy = c->p.light_max_degree == 0;
   // world > 1: the previous half's factor gathers (second stream) finish before any collective or
@@ -873,52 +875,21 @@ int half_sweep(als_ctx* c, int t) {
     HIPCHK(launch_gram(KP, S.d_X.as<float>(), S.own_n, c->slab.as<double>(), c->slab_blocks, c->d_G.as<double>(), st));
     TRYC(allreduce_G(c));
     HIPCHK(hipEventRecord(ev[1], st));
-    std::vector<double> Gf((size_t)KP * KP);
-    HIPCHK(hipMemcpyAsync(Gf.data(), c->d_G.p, Gf.size() * 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    const auto t0 = std::chrono::steady_clock::now();
-    std::vector<double> Gk((size_t)k * k), w(k), V((size_t)k * k);
-    for (int i = 0; i < k; ++i)
-      for (int j = 0; j < k; ++j) Gk[(size_t)i * k + j] = Gf[(size_t)i * KP + j];
-    S.G = Gk;
-    S.GB = S.B;
-    if (!sym_eig(k, Gk.data(), w.data(), V.data()))
-      return fail(ALS_E_NOT_POSITIVE_DEFINITE, "eigendecomposition of the Gram matrix did not converge");
-    // staging buffers live in the context: the async copies below read them after this block
-    std::vector<float>& P32 = c->h_P32;
-    std::vector<float>& lam32 = c->h_lam32;
-    P32.assign((size_t)KP * KP, 0.f);
-    lam32.assign(KP, 0.f);
-    std::vector<double> Pf((size_t)KP * KP, 0.0);
-    for (int i = 0; i < KP; ++i) Pf[(size_t)i * KP + i] = 1.0;
-    for (int i = 0; i < k; ++i)
-      for (int j = 0; j < k; ++j) Pf[(size_t)i * KP + j] = V[(size_t)i * k + j];
-    for (size_t e = 0; e < Pf.size(); ++e) P32[e] = (float)Pf[e];
-    double wmax = 0.0, wmin = INFINITY;
-    for (int i = 0; i < k; ++i) {
-      lam32[i] = (float)std::max(w[i], 0.0);
-      wmax = std::max(wmax, w[i]);
-      wmin = std::min(wmin, w[i]);
+    // eigenbasis of the src Gram on the device (eig.hip): warm-started cyclic Jacobi in fp64, no host
+    // round trip; the dst side's new basis B_t = B_s·P is formed there too
+    HIPCHK(hipMemcpyAsync(S.d_Gk.p, c->d_G.p, (size_t)KP * KP * 8, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.d_GB.p, S.d_B.p, (size_t)KP * KP * 8, hipMemcpyDeviceToDevice, st));
+    S.has_gram = true;
+    HIPCHK(launch_device_eig(KP, k, c->d_G.as<double>(), S.d_B.as<double>(), T.d_B.as<double>(), T.d_B.as<double>(),
+                             c->d_eig.as<double>(), c->d_P.as<float>(), c->d_lam.as<float>(), c->d_csmax.as<unsigned>(), st));
+    if (c->p.reg_param == 0.0) {
+      // the push-through light solve needs Λ + λn > 0 for every row; with λ = 0 a singular Gram sends
+      // every row to the explicit path (the only host round trip left, and only at regParam = 0)
+      double wmm[2] = {0.0, 0.0};
+      HIPCHK(hipMemcpyAsync(wmm, eig_minmax(c->d_eig.as<double>(), KP), 16, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (!(wmm[0] > 1e-12 * wmm[1])) force_heavy = true;
     }
-    if (!(wmin > 1e-12 * wmax) && c->p.reg_param == 0.0) force_heavy = true;
-    if (!(wmin > 1e-12 * wmax)) {
-      // the push-through form needs Λ + λn > 0 for every row; rows without positive ratings have n = 0
-      force_heavy = force_heavy || c->p.reg_param == 0.0;
-    }
-    // new basis of the dst side: B_t = B_s · P
-    std::vector<double> Bn((size_t)KP * KP, 0.0);
-    for (int i = 0; i < KP; ++i)
-      for (int m = 0; m < KP; ++m) {
-        const double b = S.B[(size_t)i * KP + m];
-        if (b == 0.0) continue;
-        const double* pr = &Pf[(size_t)m * KP];
-        double* out = &Bn[(size_t)i * KP];
-        for (int j = 0; j < KP; ++j) out[j] += b * pr[j];
-      }
-    T.B.swap(Bn);
-    eig_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    HIPCHK(hipMemcpyAsync(c->d_P.p, P32.data(), P32.size() * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(c->d_lam.p, lam32.data(), lam32.size() * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(ev[2], st));
     // world > 1: every rank rotates the whole gathered src (no collective on the critical path)
     const float* Xs = multi ? S.d_Xfull.as<float>() : S.d_X.as<float>();
@@ -928,10 +899,7 @@ int half_sweep(als_ctx* c, int t) {
       // first, from a bound: Σ_i Z_ij² = p_jᵀ G p_j, which is λ_j up to the fp32 rounding of P and of
       // the product (≤ 1e-6 λ_max), so max_i |Z_ij| ≤ √(λ_j + 1e-6 λ_max).  The split's fp16 range
       // needs the scaled maxima below 2^16; the scales put the bound at 2^13 (colscale_kernel).
-      std::vector<float>& ub = c->h_ub;
-      ub.assign(KP, 0.f);
-      for (int j = 0; j < k; ++j) ub[j] = (float)(std::sqrt(std::max(w[j], 0.0) + 1e-6 * std::max(wmax, 0.0)) * 1.001);
-      HIPCHK(hipMemcpyAsync(c->d_csmax.p, ub.data(), KP * 4, hipMemcpyHostToDevice, st));
+      // (the bound itself came from the eigensolver: launch_device_eig left it in d_csmax)
       TRYC(column_scales(c, S, T, true));
       cs_done = true;
       float sw = 1.f;
@@ -949,7 +917,7 @@ int half_sweep(als_ctx* c, int t) {
   } else {
     HIPCHK(hipEventRecord(ev[1], st));
     HIPCHK(hipMemsetAsync(c->d_lam.p, 0, KP * 4, st));
-    T.B = S.B;
+    HIPCHK(hipMemcpyAsync(T.d_B.p, S.d_B.p, (size_t)KP * KP * 8, hipMemcpyDeviceToDevice, st));
     if (c->p.reg_param == 0.0) force_heavy = true;
     HIPCHK(hipEventRecord(ev[2], st));
     if (multi) HIPCHK(hipMemcpyAsync(S.d_Z.p, S.d_Xfull.p, (size_t)S.prows() * KP * 4, hipMemcpyDeviceToDevice, st));
@@ -1026,7 +994,7 @@ int half_sweep(als_ctx* c, int t) {
   HIPCHK(hipMemcpyAsync(&err, c->d_err.p, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   T.t[ALS_T_GRAM] = event_ms(ev[0], ev[1]);
-  T.t[ALS_T_EIG] = eig_ms;
+  T.t[ALS_T_EIG] = event_ms(ev[1], ev[2]);  // device eigensolver + the new basis
   T.t[ALS_T_ROTATE] = event_ms(ev[2], ev[3]);
   T.t[ALS_T_COMM] = event_ms(ev[3], ev[4]);
   if (T.nsolve > 1) {
@@ -1053,11 +1021,8 @@ int materialize(als_ctx* c, int side) {
   if (S.orig_valid) return ALS_OK;
   if (!S.has_factors) return fail(ALS_E_STATE, "factors are not available (call fit first)");
   const int KP = c->KP;
-  std::vector<float> Bt((size_t)KP * KP);
-  for (int i = 0; i < KP; ++i)
-    for (int j = 0; j < KP; ++j) Bt[(size_t)i * KP + j] = (float)S.B[(size_t)j * KP + i];
   HIPCHK(c->d_P.ensure((size_t)KP * KP * 4));
-  HIPCHK(hipMemcpyAsync(c->d_P.p, Bt.data(), Bt.size() * 4, hipMemcpyHostToDevice, c->st));
+  HIPCHK(launch_basis_t32(S.d_B.as<double>(), c->d_P.as<float>(), KP, c->st));
   HIPCHK(S.d_orig.ensure((size_t)std::max<int64_t>(S.n, 1) * KP * 4));
   if (c->world == 1) {
     HIPCHK(launch_rotate(KP, S.d_X.as<float>(), c->d_P.as<float>(), S.d_orig.as<float>(), S.own_n, c->st));
@@ -1394,8 +1359,7 @@ int als_init_factors_random(als_ctx* c, uint64_t seed) {
     Side& S = c->s[side];
     HIPCHK(launch_init_random(c->KP, c->p.rank, S.d_X.as<float>(), S.own_n, seed + 0x51ED270B27u * (side + 1),
                               S.own0, c->st));
-    S.B.assign((size_t)c->KP * c->KP, 0.0);
-    for (int i = 0; i < c->KP; ++i) S.B[(size_t)i * c->KP + i] = 1.0;
+    HIPCHK(launch_identity(S.d_B.as<double>(), c->KP, c->st));
     S.has_factors = true;
     S.orig_valid = false;
     S.full_valid = false;
@@ -1434,22 +1398,28 @@ int als_fit(als_ctx* c) {
 int als_get_gram(als_ctx* c, int src_side, double* out) {
   if (!c || (src_side != 0 && src_side != 1) || !out) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
   const Side& S = c->s[src_side];
-  const auto& G = S.G;
-  if (G.empty()) return fail(ALS_E_STATE, "no Gram computed yet");
+  if (!S.has_gram) return fail(ALS_E_STATE, "no Gram computed yet");
+  TRYC(set_device(c));
   // G was formed from the factors in the side's basis at that time (original = X·GBᵀ):
   // YᵀY = GB G GBᵀ, restricted to the model rank (GB is the identity on the padding)
   const int k = c->p.rank, KP = c->KP;
+  std::vector<double> Gf((size_t)KP * KP), GB((size_t)KP * KP), G((size_t)k * k);
+  HIPCHK(hipMemcpyAsync(Gf.data(), S.d_Gk.p, Gf.size() * 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipMemcpyAsync(GB.data(), S.d_GB.p, GB.size() * 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  for (int i = 0; i < k; ++i)
+    for (int j = 0; j < k; ++j) G[(size_t)i * k + j] = Gf[(size_t)i * KP + j];
   std::vector<double> T((size_t)k * k, 0.0);  // T = GB_k G
   for (int i = 0; i < k; ++i)
     for (int m = 0; m < k; ++m) {
-      const double b = S.GB[(size_t)i * KP + m];
+      const double b = GB[(size_t)i * KP + m];
       if (b == 0.0) continue;
       for (int j = 0; j < k; ++j) T[(size_t)i * k + j] += b * G[(size_t)m * k + j];
     }
   for (int i = 0; i < k; ++i)
     for (int j = 0; j < k; ++j) {
       double acc = 0.0;
-      for (int m = 0; m < k; ++m) acc += T[(size_t)i * k + m] * S.GB[(size_t)j * KP + m];
+      for (int m = 0; m < k; ++m) acc += T[(size_t)i * k + m] * GB[(size_t)j * KP + m];
       out[(size_t)i * k + j] = acc;
     }
   return ALS_OK;

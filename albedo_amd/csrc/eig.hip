@@ -1,0 +1,244 @@
+// Eigenbasis of the src Gram on the device (the step between Spark's computeYtY and the per-row
+// solves, ALS.computeFactors reached from ALSRecommenderBuilder.scala:58; the engine's restatement
+// solves every row in the basis where YᵀY is diagonal, als_engine.cpp half_sweep).
+//
+// The src factors X live in an orthogonal basis B_s (original = X·B_sᵀ) and the dst side's current
+// basis B_t = B_s(prev)·P(prev) holds the eigenvectors of this side's previous Gram in original
+// coordinates, so  W = B_sᵀ·B_t  nearly diagonalises the new Gram G (the factors change little from
+// one sweep to the next):  M = Wᵀ G W  is swept by a cyclic parallel Jacobi in fp64 (one workgroup,
+// M in LDS, the 64 disjoint pairs of a round-robin round rotated at once, V = W·J accumulated in
+// global memory) until the off-diagonal mass is below 1e-30 of the diagonal's.  Then P = V, Λ = diag,
+// and the new dst basis B_t = B_s·P.  From a warm start the sweep count is small (2-4); from the
+// identity (first half-sweep) it is the usual 6-10.  Deterministic: fixed pairing, fixed order.
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdint>
+#include "device_common.h"
+#include "kernels.h"
+
+namespace albedo {
+namespace {
+
+// C = op(A)·op(B) for KP x KP fp64 row-major matrices (TA / TB: transpose), one thread per element
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void dgemm_kp_kernel(const double* __restrict__ A, const double* __restrict__ B,
+                                                       double* __restrict__ C, int KP) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= KP * KP) return;
+  const int i = e / KP, j = e % KP;
+  double acc = 0.0;
+  for (int m = 0; m < KP; ++m) {
+    const double a = TA ? A[m * KP + i] : A[i * KP + m];
+    const double b = TB ? B[j * KP + m] : B[m * KP + j];
+    acc = fma(a, b, acc);
+  }
+  C[e] = acc;
+}
+
+constexpr int JAC_THREADS = 1024;
+constexpr int JAC_MAX_SWEEPS = 30;
+
+// round r of the round-robin over n (even) players: pair i = (a, b); player n-1 is fixed
+__device__ __forceinline__ void rr_pair(int r, int i, int n, int& a, int& b) {
+  const int m = n - 1;
+  if (i == 0) {
+    a = r % m;
+    b = m;
+  } else {
+    a = (r + i) % m;
+    b = (r - i + m) % m;
+  }
+  if (a > b) { const int t = a; a = b; b = t; }
+}
+
+// M (KP x KP, global, the leading k x k block meaningful) -> eigenvalues w[0..k), V (in: W, out: W·J).
+// LDSM: M is swept in LDS (k <= 128: 129 x 128 doubles); else in place in global memory (the
+// workgroup's own stores, ordered by its barriers).
+template <bool LDSM>
+__global__ __launch_bounds__(JAC_THREADS) void jacobi_kernel(double* __restrict__ Mg, double* __restrict__ V,
+                                                             double* __restrict__ w, int k, int KP, int* __restrict__ sweeps_out) {
+  extern __shared__ double sm[];
+  __shared__ double cs[2 * 128];  // c, s of the round's pairs (k <= 256: at most 128 pairs)
+  __shared__ int pq[2 * 128];     // p, q
+  __shared__ double red[JAC_THREADS / 64][2];
+  __shared__ int done;
+  const int ld = LDSM ? k + 1 : KP;  // LDS: padded row stride (column walks spread over the banks)
+  double* M = LDSM ? sm : Mg;
+  const int tid = threadIdx.x;
+  if constexpr (LDSM)
+    for (int e = tid; e < k * k; e += JAC_THREADS) M[(e / k) * ld + e % k] = Mg[(e / k) * KP + e % k];
+  const int n = k + (k & 1);  // players; index k (odd k) is a dummy that never rotates
+  const int np = n / 2;
+  __syncthreads();
+  int sweep = 0;
+  for (; sweep < JAC_MAX_SWEEPS; ++sweep) {
+    // convergence: off-diagonal mass against the diagonal's (fixed-order block reduction)
+    double off = 0.0, dia = 0.0;
+    for (int e = tid; e < k * k; e += JAC_THREADS) {
+      const int i = e / k, j = e % k;
+      const double v = M[i * ld + j];
+      if (i == j) dia += v * v;
+      else off += v * v;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      off += __shfl_xor(off, o);
+      dia += __shfl_xor(dia, o);
+    }
+    if ((tid & 63) == 0) {
+      red[tid >> 6][0] = off;
+      red[tid >> 6][1] = dia;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double so = 0.0, sd = 0.0;
+      for (int i = 0; i < JAC_THREADS / 64; ++i) {
+        so += red[i][0];
+        sd += red[i][1];
+      }
+      done = !(so > 1e-30 * sd);
+    }
+    __syncthreads();
+    if (done) break;
+    for (int r = 0; r < n - 1; ++r) {
+      if (tid < np) {  // this round's rotation of pair tid
+        int p, q;
+        rr_pair(r, tid, n, p, q);
+        double c = 1.0, s = 0.0;
+        if (q < k) {
+          const double apq = M[p * ld + q];
+          if (apq != 0.0) {
+            const double th = (M[q * ld + q] - M[p * ld + p]) / (2.0 * apq);
+            const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(fma(th, th, 1.0)));
+            c = 1.0 / sqrt(fma(t, t, 1.0));
+            s = t * c;
+          }
+        }
+        cs[tid] = c;
+        cs[128 + tid] = s;
+        pq[tid] = p;
+        pq[128 + tid] = q < k ? q : p;  // the dummy pair rotates nothing
+      }
+      __syncthreads();
+      // rows p, q of M  (M <- Jᵀ M)
+      for (int e = tid; e < np * k; e += JAC_THREADS) {
+        const int i = e / k, j = e % k;
+        const int p = pq[i], q = pq[128 + i];
+        if (p == q) continue;
+        const double c = cs[i], s = cs[128 + i];
+        const double a = M[p * ld + j], b = M[q * ld + j];
+        M[p * ld + j] = c * a - s * b;
+        M[q * ld + j] = s * a + c * b;
+      }
+      __syncthreads();
+      // columns p, q of M (M <- M J) and of V (V <- V J)
+      for (int e = tid; e < np * k; e += JAC_THREADS) {
+        const int i = e / k, j = e % k;
+        const int p = pq[i], q = pq[128 + i];
+        if (p == q) continue;
+        const double c = cs[i], s = cs[128 + i];
+        const double a = M[j * ld + p], b = M[j * ld + q];
+        M[j * ld + p] = c * a - s * b;
+        M[j * ld + q] = s * a + c * b;
+      }
+      for (int e = tid; e < np * KP; e += JAC_THREADS) {
+        const int i = e / KP, j = e % KP;
+        const int p = pq[i], q = pq[128 + i];
+        if (p == q) continue;
+        const double c = cs[i], s = cs[128 + i];
+        const double a = V[j * KP + p], b = V[j * KP + q];
+        V[j * KP + p] = c * a - s * b;
+        V[j * KP + q] = s * a + c * b;
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < KP; i += JAC_THREADS) w[i] = i < k ? M[i * ld + i] : 0.0;
+  if (tid == 0 && sweeps_out) *sweeps_out = sweep;
+}
+
+// P32 = (float) V; lam32 = max(w, 0); ub (the rotation's column-scale bound, als_engine.cpp):
+// sqrt(max(w_j, 0) + 1e-6 max(w_max, 0)) * 1.001 as float bits; wmm = {min w, max w}
+__global__ __launch_bounds__(256) void eig_finish_kernel(const double* __restrict__ w, const double* __restrict__ V, int k,
+                                                         int KP, float* __restrict__ P32, float* __restrict__ lam32,
+                                                         unsigned* __restrict__ ub, double* __restrict__ wmm) {
+  __shared__ double smax;
+  if (threadIdx.x == 0) {
+    double mx = -INFINITY, mn = INFINITY;
+    for (int i = 0; i < k; ++i) {
+      mx = fmax(mx, w[i]);
+      mn = fmin(mn, w[i]);
+    }
+    smax = mx;
+    if (blockIdx.x == 0) {
+      wmm[0] = mn;
+      wmm[1] = mx;
+    }
+  }
+  __syncthreads();
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < KP * KP; e += gridDim.x * blockDim.x) P32[e] = (float)V[e];
+  if (blockIdx.x == 0)
+    for (int j = threadIdx.x; j < KP; j += blockDim.x) {
+      lam32[j] = j < k ? (float)fmax(w[j], 0.0) : 0.f;
+      const float u = j < k ? (float)(sqrt(fmax(w[j], 0.0) + 1e-6 * fmax(smax, 0.0)) * 1.001) : 0.f;
+      ub[j] = __float_as_uint(u);
+    }
+}
+
+__global__ void identity_kernel(double* __restrict__ B, int KP) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < KP * KP) B[e] = (e / KP == e % KP) ? 1.0 : 0.0;
+}
+
+// Bt32[i][j] = (float) B[j][i] (the rotation matrix of materialize: original = X · Bᵀ)
+__global__ void basis_t32_kernel(const double* __restrict__ B, float* __restrict__ Bt, int KP) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < KP * KP) Bt[e] = (float)B[(e % KP) * KP + e / KP];
+}
+
+}  // namespace
+
+size_t eig_scratch_doubles(int KP) { return (size_t)3 * KP * KP + KP + 2 + 2; }
+
+hipError_t launch_device_eig(int KP, int k, const double* G, const double* Bs, const double* Bt_in, double* Bt_out,
+                             double* scratch, float* P32, float* lam32, unsigned* ub, hipStream_t s) {
+  if (k < 1 || k > KP || KP > 256) return hipErrorInvalidValue;
+  double* W = scratch;               // warm start, then the eigenvectors
+  double* T = W + KP * KP;           // G·W
+  double* M = T + KP * KP;           // Wᵀ G W
+  double* w = M + KP * KP;           // eigenvalues [KP]
+  double* wmm = w + KP;              // {min, max}
+  int* sweeps = reinterpret_cast<int*>(wmm + 2);
+  const int g = (KP * KP + 255) / 256;
+  dgemm_kp_kernel<true, false><<<g, 256, 0, s>>>(Bs, Bt_in, W, KP);  // W = B_sᵀ B_t
+  dgemm_kp_kernel<false, false><<<g, 256, 0, s>>>(G, W, T, KP);
+  dgemm_kp_kernel<true, false><<<g, 256, 0, s>>>(W, T, M, KP);
+  if (k <= 128) {
+    const size_t lds = (size_t)k * (k + 1) * sizeof(double);
+    static const hipError_t attr = allow_lds(jacobi_kernel<true>, (size_t)128 * 129 * 8);
+    if (attr != hipSuccess) return attr;
+    jacobi_kernel<true><<<1, JAC_THREADS, lds, s>>>(M, W, w, k, KP, sweeps);
+  } else {
+    jacobi_kernel<false><<<1, JAC_THREADS, 0, s>>>(M, W, w, k, KP, sweeps);
+  }
+  eig_finish_kernel<<<std::max(1, std::min(64, g)), 256, 0, s>>>(w, W, k, KP, P32, lam32, ub, wmm);
+  dgemm_kp_kernel<false, false><<<g, 256, 0, s>>>(Bs, W, Bt_out, KP);  // B_t = B_s P
+  return hipGetLastError();
+}
+
+// {min w, max w} and the Jacobi sweep count of the last launch_device_eig (device pointers into scratch)
+const double* eig_minmax(const double* scratch, int KP) { return scratch + (size_t)3 * KP * KP + KP; }
+const int* eig_sweeps(const double* scratch, int KP) {
+  return reinterpret_cast<const int*>(scratch + (size_t)3 * KP * KP + KP + 2);
+}
+
+hipError_t launch_identity(double* B, int KP, hipStream_t s) {
+  identity_kernel<<<(KP * KP + 255) / 256, 256, 0, s>>>(B, KP);
+  return hipGetLastError();
+}
+
+hipError_t launch_basis_t32(const double* B, float* Bt, int KP, hipStream_t s) {
+  basis_t32_kernel<<<(KP * KP + 255) / 256, 256, 0, s>>>(B, Bt, KP);
+  return hipGetLastError();
+}
+
+}  // namespace albedo

@@ -107,6 +107,18 @@ hipError_t launch_absmax(const float* v, int64_t n, unsigned* out, hipStream_t s
 hipError_t launch_absmin(const float* v, int64_t n, unsigned* out, hipStream_t s);
 int nnls_gtile_index(int r, int c);  // block(r) >= block(c): NNLS tile layout, diagonal tiles full
 
+// Eigenbasis of the src Gram on the device (eig.hip): W = B_sᵀ·B_t_in (warm start), M = Wᵀ G W, cyclic
+// Jacobi in fp64 -> P (eigenvectors, in scratch), P32 (fp32 [KP][KP]), lam32 = max(Λ, 0), ub = the
+// rotation's column-scale bound (float bits), B_t_out = B_s·P.  G, B_s, B_t: fp64 [KP][KP] row-major
+// (B_t_in may alias B_t_out: it is read before the last GEMM writes).  scratch: eig_scratch_doubles.
+size_t eig_scratch_doubles(int KP);
+hipError_t launch_device_eig(int KP, int k, const double* G, const double* Bs, const double* Bt_in, double* Bt_out,
+                             double* scratch, float* P32, float* lam32, unsigned* ub, hipStream_t s);
+const double* eig_minmax(const double* scratch, int KP);  // device {min Λ, max Λ} of the last call
+const int* eig_sweeps(const double* scratch, int KP);     // device Jacobi sweep count of the last call
+hipError_t launch_identity(double* B, int KP, hipStream_t s);
+hipError_t launch_basis_t32(const double* B, float* Bt, int KP, hipStream_t s);  // Bt = (float) Bᵀ
+
 // Seeded unit-norm Gaussian rows (global row index row0 + r) for large synthetic runs.
 hipError_t launch_init_random(int KP, int kreal, float* X, int64_t n, uint64_t seed, int64_t row0, hipStream_t s);
 

@@ -37,6 +37,7 @@ for s in "$@"; do
     trace_c5) mkdir -p gpurun_out/trace_c5 && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_c5 -o run -- python3 -u bench.py --config c5 --steps 1 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/trace_c5/bench.json 2> gpurun_out/trace_c5/bench.err ;;
     tests_mr) timeout -k 10 900 $PYT tests/test_multi_rank.py > gpurun_out/tests_mr.log 2>&1 ;;
     wavetime) (cd tools/probe && timeout -k 5 120 ./wavetime 20000000 80,160,320,640,1280,4096 200000000 && timeout -k 5 120 ./wavetime_bo 20000000 80,160,320,640,1280,4096 200000000) > gpurun_out/wavetime.txt 2>&1 ;;
+    c1p) timeout -k 10 900 python -u tools/c1p_job.py --out gpurun_out/c1p_job.json > gpurun_out/c1p_job.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
