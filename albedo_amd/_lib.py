@@ -112,6 +112,7 @@ SIGNATURES = [
     ("als_set_ratings_synthetic", C.c_int, [P, C.c_uint64, C.c_int32, C.c_int64, C.c_int64, I64P, F64P, I32P]),
     ("als_comm_init_host", C.c_int, [P, C.c_int32, C.c_int32, ALLREDUCE_FN, ALLGATHER_FN, P]),
     ("als_host_eigh", C.c_int, [C.c_int32, F64P, F64P, F64P]),
+    ("als_device_eigh", C.c_int, [C.c_int32, C.c_int32, F64P, F64P, F64P, F64P, I32P]),
     ("als_host_spark_side_seeds", C.c_int, [C.c_int64, I64P, I64P]),
     ("als_host_spark_init", C.c_int, [I32P, C.c_int64, C.c_int32, C.c_int64, C.c_int32, F32P]),
     ("als_host_plan_shards", C.c_int, [I64P, C.c_int64, C.c_int32, I64P]),

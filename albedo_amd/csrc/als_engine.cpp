@@ -990,9 +990,12 @@ int half_sweep(als_ctx* c, int t) {
     HIPCHK(hipEventRecord(c->evc[8], c->st2));
   }
   HIPCHK(hipEventRecord(ev[6], st));
-  int err = 0;
+  int err = 0, sweeps = 0;
   HIPCHK(hipMemcpyAsync(&err, c->d_err.p, 4, hipMemcpyDeviceToHost, st));
+  if (c->p.implicit_prefs) HIPCHK(hipMemcpyAsync(&sweeps, eig_sweeps(c->d_eig.as<double>(), KP), 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  T.solver[0] = sweeps;  // Cholesky path: the device eigensolver's Jacobi sweeps (als_solver_stats)
+  T.solver[1] = T.solver[2] = T.solver[3] = 0;
   T.t[ALS_T_GRAM] = event_ms(ev[0], ev[1]);
   T.t[ALS_T_EIG] = event_ms(ev[1], ev[2]);  // device eigensolver + the new basis
   T.t[ALS_T_ROTATE] = event_ms(ev[2], ev[3]);
@@ -1008,7 +1011,8 @@ int half_sweep(als_ctx* c, int t) {
   if (err & 3)
     return fail(ALS_E_NOT_POSITIVE_DEFINITE,
                 "LAPACK.dppsv-equivalent Cholesky met a non-positive pivot because A is not positive "
-                "definite. Is A derived from a singular matrix (e.g. collinear column values)?");
+                "definite. Is A derived from a singular matrix (e.g. collinear column values)? (flags " +
+                    std::to_string(err) + ", " + std::to_string(sweeps) + " eigensolver sweeps)");
   T.has_factors = true;
   T.orig_valid = false;
   T.full_valid = multi;  // gathered behind the solve (st2); the next half waits for it
@@ -2064,6 +2068,46 @@ int als_set_ratings_synthetic(als_ctx* c, uint64_t seed, int32_t rounds, int64_t
 int als_host_eigh(int32_t n, const double* a, double* w, double* v) {
   if (n <= 0 || !a || !w || !v) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
   if (!sym_eig(n, a, w, v)) return fail(ALS_E_NOT_POSITIVE_DEFINITE, "eigensolver did not converge");
+  return ALS_OK;
+}
+
+int als_device_eigh(int32_t device, int32_t k, const double* g, const double* w0, double* w, double* v,
+                    int32_t* sweeps) {
+  if (k <= 0 || k > 256 || !g || !w || !v) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  if (hipSetDevice(device) != hipSuccess) return fail(ALS_E_NO_DEVICE, "no such device");
+  const int KP = padded_rank(k);
+  std::vector<double> G((size_t)KP * KP, 0.0), B((size_t)KP * KP, 0.0), W((size_t)KP * KP, 0.0);
+  for (int i = 0; i < KP; ++i) B[(size_t)i * KP + i] = W[(size_t)i * KP + i] = 1.0;
+  for (int i = 0; i < k; ++i)
+    for (int j = 0; j < k; ++j) {
+      G[(size_t)i * KP + j] = g[(size_t)i * k + j];
+      if (w0) W[(size_t)i * KP + j] = w0[(size_t)i * k + j];
+    }
+  DevBuf dG, dB, dW, dOut, dS, dP, dl, du;
+  HIPCHK(dG.ensure(G.size() * 8));
+  HIPCHK(dB.ensure(B.size() * 8));
+  HIPCHK(dW.ensure(W.size() * 8));
+  HIPCHK(dOut.ensure(W.size() * 8));
+  HIPCHK(dS.ensure(eig_scratch_doubles(KP) * 8));
+  HIPCHK(dP.ensure((size_t)KP * KP * 4));
+  HIPCHK(dl.ensure((size_t)KP * 4));
+  HIPCHK(du.ensure((size_t)KP * 4));
+  HIPCHK(hipMemcpy(dG.p, G.data(), G.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dB.p, B.data(), B.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dW.p, W.data(), W.size() * 8, hipMemcpyHostToDevice));
+  // B_s = I, B_t = W0: the warm start is W0 itself; B_t_out = P
+  HIPCHK(launch_device_eig(KP, k, dG.as<double>(), dB.as<double>(), dW.as<double>(), dOut.as<double>(), dS.as<double>(),
+                           dP.as<float>(), dl.as<float>(), du.as<unsigned>(), nullptr));
+  std::vector<double> wk(KP), P(W.size());
+  int sw = 0;
+  HIPCHK(hipMemcpy(P.data(), dOut.p, P.size() * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(wk.data(), dS.as<double>() + (size_t)3 * KP * KP, KP * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&sw, eig_sweeps(dS.as<double>(), KP), 4, hipMemcpyDeviceToHost));
+  for (int i = 0; i < k; ++i) {
+    w[i] = wk[i];
+    for (int j = 0; j < k; ++j) v[(size_t)i * k + j] = P[(size_t)i * KP + j];
+  }
+  if (sweeps) *sweeps = sw;
   return ALS_OK;
 }
 

@@ -51,11 +51,12 @@ __device__ __forceinline__ void rr_pair(int r, int i, int n, int& a, int& b) {
   if (a > b) { const int t = a; a = b; b = t; }
 }
 
-// M (KP x KP, global, the leading k x k block meaningful) -> eigenvalues w[0..k), V (in: W, out: W·J).
+// M (KP x KP, global, the leading k x k block meaningful) -> eigenvalues w[0..k), VT = Vᵀ (in: Wᵀ,
+// out: (W·J)ᵀ = Jᵀ·Wᵀ: the rotations act on rows of VT, contiguous in memory).
 // LDSM: M is swept in LDS (k <= 128: 129 x 128 doubles); else in place in global memory (the
 // workgroup's own stores, ordered by its barriers).
 template <bool LDSM>
-__global__ __launch_bounds__(JAC_THREADS) void jacobi_kernel(double* __restrict__ Mg, double* __restrict__ V,
+__global__ __launch_bounds__(JAC_THREADS) void jacobi_kernel(double* __restrict__ Mg, double* __restrict__ VT,
                                                              double* __restrict__ w, int k, int KP, int* __restrict__ sweeps_out) {
   extern __shared__ double sm[];
   __shared__ double cs[2 * 128];  // c, s of the round's pairs (k <= 256: at most 128 pairs)
@@ -95,7 +96,7 @@ __global__ __launch_bounds__(JAC_THREADS) void jacobi_kernel(double* __restrict_
         so += red[i][0];
         sd += red[i][1];
       }
-      done = !(so > 1e-30 * sd);
+      done = !(so > 1e-18 * sd);  // off-diagonal norm <= 1e-9 of the diagonal's (P is used in fp32)
     }
     __syncthreads();
     if (done) break;
@@ -140,14 +141,14 @@ __global__ __launch_bounds__(JAC_THREADS) void jacobi_kernel(double* __restrict_
         M[j * ld + p] = c * a - s * b;
         M[j * ld + q] = s * a + c * b;
       }
-      for (int e = tid; e < np * KP; e += JAC_THREADS) {
+      for (int e = tid; e < np * KP; e += JAC_THREADS) {  // VT = Vᵀ: rows p, q (contiguous)
         const int i = e / KP, j = e % KP;
         const int p = pq[i], q = pq[128 + i];
         if (p == q) continue;
         const double c = cs[i], s = cs[128 + i];
-        const double a = V[j * KP + p], b = V[j * KP + q];
-        V[j * KP + p] = c * a - s * b;
-        V[j * KP + q] = s * a + c * b;
+        const double a = VT[p * KP + j], b = VT[q * KP + j];
+        VT[p * KP + j] = c * a - s * b;
+        VT[q * KP + j] = s * a + c * b;
       }
       __syncthreads();
     }
@@ -156,9 +157,122 @@ __global__ __launch_bounds__(JAC_THREADS) void jacobi_kernel(double* __restrict_
   if (tid == 0 && sweeps_out) *sweeps_out = sweep;
 }
 
+// k <= 128: JAC_WG workgroups sweep identical copies of M in LDS (same code, same inputs, fixed
+// order: bit-identical rotations) and each applies the rotations to its own JAC_WG-th of the columns of
+// VT, also in LDS, so no global memory is touched inside the sweeps.  One round = the rotations of the
+// round's disjoint pairs computed from M, a barrier, then M <- Jᵀ M J as 2 x 2 blocks (pair a's rows x
+// pair b's columns: both sides of the similarity in one pass) and VT's rows, a barrier.
+constexpr int JAC_WG = 8;
+__global__ __launch_bounds__(JAC_THREADS) void jacobi_lds_kernel(const double* __restrict__ Mg, double* __restrict__ VTg,
+                                                                 double* __restrict__ w, int k, int KP,
+                                                                 int* __restrict__ sweeps_out) {
+  extern __shared__ double sm[];
+  __shared__ double cs[2 * 64];
+  __shared__ int pq[2 * 64];
+  __shared__ double red[JAC_THREADS / 64][2];
+  __shared__ int done;
+  const int ld = k + 1;           // M row stride (column walks spread over the banks)
+  const int nc = KP / JAC_WG;     // VT columns of this workgroup
+  const int c0 = blockIdx.x * nc;
+  double* M = sm;
+  double* VT = sm + k * ld;       // [KP][nc]
+  const int tid = threadIdx.x;
+  for (int e = tid; e < k * k; e += JAC_THREADS) M[(e / k) * ld + e % k] = Mg[(e / k) * KP + e % k];
+  for (int e = tid; e < KP * nc; e += JAC_THREADS) VT[e] = VTg[(e / nc) * KP + c0 + e % nc];
+  const int n = k + (k & 1);  // players; index k (odd k) is a dummy that never rotates
+  const int np = n / 2;
+  __syncthreads();
+  int sweep = 0;
+  for (; sweep < JAC_MAX_SWEEPS; ++sweep) {
+    double off = 0.0, dia = 0.0;
+    for (int e = tid; e < k * k; e += JAC_THREADS) {
+      const int i = e / k, j = e % k;
+      const double v = M[i * ld + j];
+      if (i == j) dia += v * v;
+      else off += v * v;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      off += __shfl_xor(off, o);
+      dia += __shfl_xor(dia, o);
+    }
+    if ((tid & 63) == 0) {
+      red[tid >> 6][0] = off;
+      red[tid >> 6][1] = dia;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double so = 0.0, sd = 0.0;
+      for (int i = 0; i < JAC_THREADS / 64; ++i) {
+        so += red[i][0];
+        sd += red[i][1];
+      }
+      // off-diagonal norm <= 1e-9 of the diagonal's: P is used in fp32 (its rounding is 6e-8)
+      done = !(so > 1e-18 * sd);
+    }
+    __syncthreads();
+    if (done) break;
+    for (int r = 0; r < n - 1; ++r) {
+      if (tid < np) {
+        int p, q;
+        rr_pair(r, tid, n, p, q);
+        double c = 1.0, s = 0.0;
+        if (q < k) {
+          const double apq = M[p * ld + q];
+          if (apq != 0.0) {
+            const double th = (M[q * ld + q] - M[p * ld + p]) / (2.0 * apq);
+            const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(fma(th, th, 1.0)));
+            c = 1.0 / sqrt(fma(t, t, 1.0));
+            s = t * c;
+          }
+        }
+        cs[tid] = c;
+        cs[64 + tid] = s;
+        pq[tid] = p;
+        pq[64 + tid] = q;  // q = k: the dummy (odd k), its row / column do not exist
+      }
+      __syncthreads();
+      // M <- Jᵀ M J on 2 x 2 blocks: rows {pa, qa} x columns {pb, qb}
+      for (int e = tid; e < np * np; e += JAC_THREADS) {
+        const int ia = e / np, ib = e % np;
+        const int pa = pq[ia], qa = pq[64 + ia], pb = pq[ib], qb = pq[64 + ib];
+        const double ca = cs[ia], sa = cs[64 + ia], cb = cs[ib], sb = cs[64 + ib];
+        const bool ha = qa < k, hb = qb < k;
+        const double m00 = M[pa * ld + pb];
+        const double m01 = hb ? M[pa * ld + qb] : 0.0;
+        const double m10 = ha ? M[qa * ld + pb] : 0.0;
+        const double m11 = (ha && hb) ? M[qa * ld + qb] : 0.0;
+        // rows: [r0; r1] = [ca -sa; sa ca] [m0x; m1x]
+        const double r00 = ca * m00 - sa * m10, r01 = ca * m01 - sa * m11;
+        const double r10 = sa * m00 + ca * m10, r11 = sa * m01 + ca * m11;
+        // columns: [x0 x1] [cb sb; -sb cb]
+        M[pa * ld + pb] = r00 * cb - r01 * sb;
+        if (hb) M[pa * ld + qb] = r00 * sb + r01 * cb;
+        if (ha) M[qa * ld + pb] = r10 * cb - r11 * sb;
+        if (ha && hb) M[qa * ld + qb] = r10 * sb + r11 * cb;
+      }
+      // VT <- Jᵀ VT: rows pa, qa of this workgroup's columns
+      for (int e = tid; e < np * nc; e += JAC_THREADS) {
+        const int ia = e / nc, j = e % nc;
+        const int pa = pq[ia], qa = pq[64 + ia];
+        if (qa >= k) continue;
+        const double ca = cs[ia], sa = cs[64 + ia];
+        const double a = VT[pa * nc + j], b = VT[qa * nc + j];
+        VT[pa * nc + j] = ca * a - sa * b;
+        VT[qa * nc + j] = sa * a + ca * b;
+      }
+      __syncthreads();
+    }
+  }
+  for (int e = tid; e < KP * nc; e += JAC_THREADS) VTg[(e / nc) * KP + c0 + e % nc] = VT[e];
+  if (blockIdx.x == 0) {
+    for (int i = tid; i < KP; i += JAC_THREADS) w[i] = i < k ? M[i * ld + i] : 0.0;
+    if (tid == 0 && sweeps_out) *sweeps_out = sweep;
+  }
+}
+
 // P32 = (float) V; lam32 = max(w, 0); ub (the rotation's column-scale bound, als_engine.cpp):
 // sqrt(max(w_j, 0) + 1e-6 max(w_max, 0)) * 1.001 as float bits; wmm = {min w, max w}
-__global__ __launch_bounds__(256) void eig_finish_kernel(const double* __restrict__ w, const double* __restrict__ V, int k,
+__global__ __launch_bounds__(256) void eig_finish_kernel(const double* __restrict__ w, const double* __restrict__ VT, int k,
                                                          int KP, float* __restrict__ P32, float* __restrict__ lam32,
                                                          unsigned* __restrict__ ub, double* __restrict__ wmm) {
   __shared__ double smax;
@@ -175,7 +289,8 @@ __global__ __launch_bounds__(256) void eig_finish_kernel(const double* __restric
     }
   }
   __syncthreads();
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < KP * KP; e += gridDim.x * blockDim.x) P32[e] = (float)V[e];
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < KP * KP; e += gridDim.x * blockDim.x)
+    P32[e] = (float)VT[(e % KP) * KP + e / KP];  // P = V = VTᵀ
   if (blockIdx.x == 0)
     for (int j = threadIdx.x; j < KP; j += blockDim.x) {
       lam32[j] = j < k ? (float)fmax(w[j], 0.0) : 0.f;
@@ -202,26 +317,26 @@ size_t eig_scratch_doubles(int KP) { return (size_t)3 * KP * KP + KP + 2 + 2; }
 hipError_t launch_device_eig(int KP, int k, const double* G, const double* Bs, const double* Bt_in, double* Bt_out,
                              double* scratch, float* P32, float* lam32, unsigned* ub, hipStream_t s) {
   if (k < 1 || k > KP || KP > 256) return hipErrorInvalidValue;
-  double* W = scratch;               // warm start, then the eigenvectors
-  double* T = W + KP * KP;           // G·W
+  double* WT = scratch;              // Wᵀ (warm start), then Vᵀ
+  double* T = WT + KP * KP;          // G·W
   double* M = T + KP * KP;           // Wᵀ G W
   double* w = M + KP * KP;           // eigenvalues [KP]
   double* wmm = w + KP;              // {min, max}
   int* sweeps = reinterpret_cast<int*>(wmm + 2);
   const int g = (KP * KP + 255) / 256;
-  dgemm_kp_kernel<true, false><<<g, 256, 0, s>>>(Bs, Bt_in, W, KP);  // W = B_sᵀ B_t
-  dgemm_kp_kernel<false, false><<<g, 256, 0, s>>>(G, W, T, KP);
-  dgemm_kp_kernel<true, false><<<g, 256, 0, s>>>(W, T, M, KP);
+  dgemm_kp_kernel<true, false><<<g, 256, 0, s>>>(Bt_in, Bs, WT, KP);  // Wᵀ = B_tᵀ B_s
+  dgemm_kp_kernel<false, true><<<g, 256, 0, s>>>(G, WT, T, KP);      // G W
+  dgemm_kp_kernel<false, false><<<g, 256, 0, s>>>(WT, T, M, KP);     // Wᵀ G W
   if (k <= 128) {
-    const size_t lds = (size_t)k * (k + 1) * sizeof(double);
-    static const hipError_t attr = allow_lds(jacobi_kernel<true>, (size_t)128 * 129 * 8);
+    const size_t lds = ((size_t)k * (k + 1) + (size_t)KP * (KP / JAC_WG)) * sizeof(double);
+    static const hipError_t attr = allow_lds(jacobi_lds_kernel, ((size_t)128 * 129 + 128 * 16) * 8);
     if (attr != hipSuccess) return attr;
-    jacobi_kernel<true><<<1, JAC_THREADS, lds, s>>>(M, W, w, k, KP, sweeps);
+    jacobi_lds_kernel<<<JAC_WG, JAC_THREADS, lds, s>>>(M, WT, w, k, KP, sweeps);
   } else {
-    jacobi_kernel<false><<<1, JAC_THREADS, 0, s>>>(M, W, w, k, KP, sweeps);
+    jacobi_kernel<false><<<1, JAC_THREADS, 0, s>>>(M, WT, w, k, KP, sweeps);
   }
-  eig_finish_kernel<<<std::max(1, std::min(64, g)), 256, 0, s>>>(w, W, k, KP, P32, lam32, ub, wmm);
-  dgemm_kp_kernel<false, false><<<g, 256, 0, s>>>(Bs, W, Bt_out, KP);  // B_t = B_s P
+  eig_finish_kernel<<<std::max(1, std::min(64, g)), 256, 0, s>>>(w, WT, k, KP, P32, lam32, ub, wmm);
+  dgemm_kp_kernel<false, true><<<g, 256, 0, s>>>(Bs, WT, Bt_out, KP);  // B_t = B_s P = B_s (Vᵀ)ᵀ
   return hipGetLastError();
 }
 

@@ -121,9 +121,13 @@ def main():
         stage[0] += tt
     barrier()
     elapsed = time.perf_counter() - t_start
-    nnls_iters = {}
+    nnls_iters, eig_sweeps = {}, {}
     for side in (0, 1):
         L.check(lib.als_path_stats(h, side, L.ptr(stats[side], C.c_int64)))
+        if args.config not in NONNEGATIVE:
+            sv = np.zeros(4, np.int64)
+            L.check(lib.als_solver_stats(h, side, L.ptr(sv, C.c_int64)))
+            eig_sweeps["user" if side == 0 else "item"] = int(sv[0])
         if args.config in NONNEGATIVE:
             sv = np.zeros(4, np.int64)
             L.check(lib.als_solver_stats(h, side, L.ptr(sv, C.c_int64)))
@@ -247,6 +251,7 @@ def main():
                                     for s in (0, 1) for i, n in enumerate(L.T_NAMES[:7])},
             "paths": {"user": stats[0].tolist(), "item": stats[1].tolist()},
             "nnls_iterations_last_sweep": nnls_iters or None,
+            "eig_jacobi_sweeps_last_sweep": eig_sweeps or None,
             "setup_s": setup_s,
         }
         print(json.dumps(line), flush=True)

@@ -205,6 +205,11 @@ int als_comm_init_host(als_ctx* ctx, int32_t rank, int32_t world, int (*allreduc
 
 /* ---- host-only utilities (no GPU; exercised by the CPU test suite) ----------------------------- */
 int als_host_eigh(int32_t n, const double* a, double* w, double* v);  /* a = v diag(w) vᵀ, w ascending */
+/* The engine's device eigensolver (warm-started cyclic Jacobi, eig.hip) on one k x k symmetric g:
+ * a = v diag(w) vᵀ, w unordered; w0 (or NULL = identity) the orthogonal warm start; sweeps: Jacobi
+ * sweeps taken.  Test hook, like als_host_eigh. */
+int als_device_eigh(int32_t device, int32_t k, const double* g, const double* w0, double* w, double* v,
+                    int32_t* sweeps);
 int als_host_spark_side_seeds(int64_t seed, int64_t* user_seed, int64_t* item_seed);
 int als_host_spark_init(const int32_t* ids_sorted, int64_t n, int32_t rank, int64_t side_seed,
                         int32_t num_blocks, float* out);

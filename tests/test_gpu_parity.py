@@ -781,3 +781,36 @@ def test_nnls_lockstep_light_rows(gpu_lib, monkeypatch, k, wgs):
     assert np.all(U >= 0)
     assert _rel(U, U_ref) < 1e-3
     assert np.mean((U == 0) == (U_ref == 0)) > 0.995
+
+
+@pytest.mark.parametrize("k", [50, 128, 200])
+def test_device_eigensolver(gpu_lib, k):
+    """The half-sweep's device eigensolver (eig.hip, warm-started cyclic Jacobi in fp64) on Grams of
+    factor-like rows whose columns span 3.5 decades (eigenvalues over 7): eigenvalues equal LAPACK's,
+    V orthogonal, VᵀGV diagonal to fp64 precision, cold and warm-started from the eigenvectors of a
+    nearby Gram (the next sweep's situation), with the warm start taking few sweeps."""
+    from albedo_amd import _lib as L
+    rng = np.random.default_rng(k)
+    X = rng.standard_normal((20000, k)) * np.logspace(0, 3.5, k)
+    G = X.T @ X
+    X2 = X + 0.01 * rng.standard_normal(X.shape) * np.logspace(0, 3.5, k)
+    G2 = X2.T @ X2
+    ref = np.linalg.eigvalsh(G)
+    out = {}
+    for name, g, w0 in (("cold", G, None), ("warm", G2, "cold")):
+        w = np.empty(k)
+        V = np.empty((k, k))
+        sw = np.zeros(1, np.int32)
+        W0 = None if w0 is None else np.ascontiguousarray(out[w0][1])
+        L.check(gpu_lib.als_device_eigh(0, k, L.ptr(np.ascontiguousarray(g), C.c_double),
+                                        None if W0 is None else L.ptr(W0, C.c_double), L.ptr(w, C.c_double),
+                                        L.ptr(V, C.c_double), L.ptr(sw, C.c_int32)))
+        out[name] = (w, V, int(sw[0]))
+        # the solver stops once the off-diagonal mass is below 1e-9 of the diagonal's (Frobenius): P
+        # is used in fp32, whose rounding is 6e-8
+        gn = np.linalg.norm(g)
+        assert np.abs(V.T @ V - np.eye(k)).max() < 1e-12, name
+        assert np.linalg.norm(V.T @ g @ V - np.diag(w)) < 2e-9 * gn, name
+        assert np.abs(np.sort(w) - np.linalg.eigvalsh(g)).max() < 2e-9 * gn, name
+    assert np.abs(np.sort(out["cold"][0]) - ref).max() < 2e-9 * np.linalg.norm(G)
+    assert out["cold"][2] <= 12 and out["warm"][2] <= out["cold"][2], (out["cold"][2], out["warm"][2])

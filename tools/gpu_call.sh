@@ -38,6 +38,8 @@ for s in "$@"; do
     tests_mr) timeout -k 10 900 $PYT tests/test_multi_rank.py > gpurun_out/tests_mr.log 2>&1 ;;
     wavetime) (cd tools/probe && timeout -k 5 120 ./wavetime 20000000 80,160,320,640,1280,4096 200000000 && timeout -k 5 120 ./wavetime_bo 20000000 80,160,320,640,1280,4096 200000000) > gpurun_out/wavetime.txt 2>&1 ;;
     c1p) timeout -k 10 900 python -u tools/c1p_job.py --out gpurun_out/c1p_job.json > gpurun_out/c1p_job.log 2>&1 ;;
+    tests_eig) timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "device_eigensolver or half_sweep_ranks" > gpurun_out/tests_eig.log 2>&1 ;;
+    bench_c4q) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 > gpurun_out/bench_c4q.json 2> gpurun_out/bench_c4q.err ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
