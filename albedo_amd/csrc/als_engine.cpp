@@ -313,37 +313,20 @@ int split_chunk_len() {
 // for degrees up to nnls_batch_max_degree(KP, slots).  A lockstep iteration costs about the same for
 // any slot count, so the variants pay off down to 8 slots (KP = 256 per row-iteration, tools/probe/
 // batchtime: 16 slots 1.3 us, 8 slots 2.2 us, 4 slots 4.7 us against 4.5 us for solve_nnls_kernel);
-// ALBEDO_NNLS_MINSLOTS=s moves the floor (default 8), ALBEDO_NNLS_BATCH=0 sends every row to
-// solve_nnls_kernel (A/B measurements).
+// rows of higher degree take solve_nnls_kernel.
 constexpr int BATCH_SLOTS[5] = {16, 8, 4, 2, 1};
+constexpr int BATCH_MIN_SLOTS = 8;
 int64_t nnls_batch_rows_limit(const als_ctx* c, int v) {
-  static const int minslots = [] {
-    const char* e = std::getenv("ALBEDO_NNLS_BATCH");
-    if (e && std::strcmp(e, "0") == 0) return 1 << 20;
-    const char* m = std::getenv("ALBEDO_NNLS_MINSLOTS");
-    return (m && std::atoi(m) > 0) ? std::atoi(m) : 8;
-  }();
-  if (BATCH_SLOTS[v] < minslots) return 0;
+  if (BATCH_SLOTS[v] < BATCH_MIN_SLOTS) return 0;
   return std::min<int64_t>(nnls_batch_max_degree(c->KP, BATCH_SLOTS[v]), light_limit(c));
 }
 
 // world > 1: the solve runs in this many row chunks, each gathered on a second stream while the
-// next one solves; ALBEDO_GATHER_CHUNKS overrides (1..8).
-int gather_chunk_count() {
-  const char* e = std::getenv("ALBEDO_GATHER_CHUNKS");
-  const int n = (e && *e) ? std::atoi(e) : 4;
-  return std::max(1, std::min(8, n));
-}
+// next one solves
+int gather_chunk_count() { return 4; }
 
-// Light rows of degree <= 16 take light16.hip (pairs of degree <= 8 rows, then singles) unless
-// ALBEDO_LIGHT16=0 (the generic solve_light_kernel<KP, 16>: A/B)
-bool light16_on() {
-  static const bool on = [] { const char* e = std::getenv("ALBEDO_LIGHT16"); return !(e && e[0] == '0'); }();
-  return on;
-}
-
-// Heavy rows at padded rank <= 128 run one wave per row (heavy_wave.hip) unless ALBEDO_HEAVY=wg
-// selects the 4-wave workgroup kernel (A/B measurements); rank 256 always uses the workgroup kernel.
+// Heavy rows at padded rank <= 128 run one wave per row (heavy_wave.hip); rank 256 uses the 4-wave
+// workgroup kernel (solve_heavy_kernel).
 bool use_wave_kernel(const als_ctx* c);
 
 int factor_buffers(als_ctx* c);
@@ -653,29 +636,19 @@ int column_scales(als_ctx* c, const Side& S, const Side& T, bool have_max = fals
 int heavy_launches(als_ctx* c, const Side& T, SolveArgs a, int64_t h0, int64_t hn, bool nnls, int q = 0);
 bool use_wave_kernel(const als_ctx* c);
 
-// KP = 128: the rotation on bf16 MFMA with the fused operand split (rotate_bf); ALBEDO_ROTATE_BF=0
-// keeps the fp32 MFMA rotation + colmax epilogue + separate presplit pass (A/B)
-bool rotate_bf_on(const als_ctx* c) {
-  static const bool off = [] {
-    const char* e = std::getenv("ALBEDO_ROTATE_BF");
-    return e && std::atoi(e) == 0;
-  }();
-  return !off && c->KP == 128;
-}
+// KP = 128: the rotation on bf16 MFMA with the fused operand split (rotate_bf); KP = 64 / 256 keep the
+// fp32 MFMA rotation + colmax epilogue + separate presplit pass
+bool rotate_bf_on(const als_ctx* c) { return c->KP == 128; }
 
 // One confidence c for every rating of dst side T (explicit: c = 1; implicit: all |r| equal): the
 // heavy build's operand split z·√c·colscale -> fp16 hi + lo is then the same for every gather of a
 // src row, so it runs once per src row here (launch_presplit) instead of once per gathered rating
-// inside the wave kernel.  ALBEDO_PRESPLIT=0 keeps the per-rating split (A/B).
+// inside the wave kernel.
 // presplit_wanted: whether the split applies to this half (and its √c); split_done: the rotation
 // already wrote it (rotate_bf)
 bool presplit_wanted(const als_ctx* c, const Side& T, float* sw) {
-  static const bool off = [] {
-    const char* e = std::getenv("ALBEDO_PRESPLIT");
-    return e && std::atoi(e) == 0;
-  }();
   const bool uniform = !c->p.implicit_prefs || (T.vmin == T.vmax && T.vmax > 0.f);
-  if (off || !uniform || !use_wave_kernel(c) || T.boff[NBUCKET] == T.boff[B_HEAVY]) return false;
+  if (!uniform || !use_wave_kernel(c) || T.boff[NBUCKET] == T.boff[B_HEAVY]) return false;
   const float cw = c->p.implicit_prefs ? (float)c->p.alpha * T.vmax : 1.0f;
   if (!(cw > 0.f)) return false;
   *sw = std::sqrt(cw);
@@ -843,13 +816,7 @@ int heavy_launches(als_ctx* c, const Side& T, SolveArgs a, int64_t h0, int64_t h
   return ALS_OK;
 }
 
-bool use_wave_kernel(const als_ctx* c) {
-  static const bool wg = [] {
-    const char* e = std::getenv("ALBEDO_HEAVY");
-    return e && std::strcmp(e, "wg") == 0;
-  }();
-  return c->KP <= 128 && !wg;
-}
+bool use_wave_kernel(const als_ctx* c) { return c->KP <= 128; }
 
 int half_sweep(als_ctx* c, int t) {
   const int sidx = 1 - t;
@@ -966,7 +933,7 @@ int half_sweep(als_ctx* c, int t) {
       a.n_rows = T.cb[b][q + 1] - T.cb[b][q];
       if (force_heavy && use_wave_kernel(c)) HIPCHK(launch_solve_wave(KP, a, st));
       else if (force_heavy) HIPCHK(launch_solve_heavy(KP, a, st));
-      else if (b == B_L16 && light16_on()) {  // degree <= 8: two rows per wave unit, then the rest
+      else if (b == B_L16) {  // light16.hip: degree <= 8 two rows per wave unit, then the rest
         SolveArgs p8 = a, p16 = a;
         p8.n_rows = T.c8[q];
         p16.rows += T.c8[q];
@@ -1492,18 +1459,6 @@ int als_model_create(int32_t rank, int64_t nu, const int32_t* uids, const float*
   return ALS_OK;
 }
 
-// top-k experiment switches, read once: ALBEDO_TOPK_DRAIN=1 (wait for every DMA each chunk),
-// ALBEDO_TOPK_THR0=0 (no starting thresholds), ALBEDO_TOPK_PRUNE=0 (no chunk bound: every chunk)
-struct TopkKnobs {
-  int drain = 0;
-  bool thr0 = true, prune = true;
-  TopkKnobs() {
-    if (const char* e = std::getenv("ALBEDO_TOPK_DRAIN")) drain = std::atoi(e);
-    if (const char* e = std::getenv("ALBEDO_TOPK_THR0")) thr0 = std::atoi(e) != 0;
-    if (const char* e = std::getenv("ALBEDO_TOPK_PRUNE")) prune = std::atoi(e) != 0;
-  }
-};
-
 // One recommendForAll* call's prepared dst side (topk.hip): max row norms (the pre-selection's error
 // bound), fp16 power-of-two scales, the descending-norm fp16 image with chunk head norms, dst ids on
 // the device; plus the per-chunk scratch reused by every src chunk.
@@ -1545,15 +1500,8 @@ int topk_dst_basis(als_ctx* c, const Side& T, TopkPlan& P, std::vector<double>& 
 // The scan prunes against the kt-th best candidate so far, not the 64th: certification needs a gap
 // between the k-th exact score and the kt-th approximate one (~1e-3 relative), and k + 16 leaves one
 // while the threshold rises faster than at 64 (fewer dst chunks scanned once the factors converge).
-// The lists still hold 64 and the best 64 are rescored.  ALBEDO_TOPK_KT overrides (k .. 64).
-int topk_threshold_rank(int k) {
-  static const int env = [] {
-    const char* e = std::getenv("ALBEDO_TOPK_KT");
-    return e ? std::atoi(e) : 0;
-  }();
-  const int kt = env > 0 ? env : k + 16;
-  return std::max(k, std::min(TOPK_KC, kt));
-}
+// The lists still hold 64 and the best 64 are rescored.
+int topk_threshold_rank(int k) { return std::max(k, std::min(TOPK_KC, k + 16)); }
 
 int topk_plan(als_ctx* c, int src, int k, TopkPlan& P) {
   P.src = src;
@@ -1587,13 +1535,12 @@ int topk_plan(als_ctx* c, int src, int k, TopkPlan& P) {
   P.tsc = pow2_scale(P.tmax);
   // dst side in descending-norm order, fp16 rows + chunk head norms (also for k > 64: the exact scan
   // visits the dst rows in this norm order and stops early)
-  static const TopkKnobs tk;
   P.CH = topk_chunk_rows(KP);
   P.n_chunks = (T.n + P.CH - 1) / P.CH;
   P.n_super = (P.n_chunks + TOPK_SUPER - 1) / TOPK_SUPER;
   // the chunk bound prunes only catalogues larger than the candidate lists (smaller ones are scanned
   // whole: the lists then hold every dst row, which select's n_dst <= TOPK_KC shortcut relies on)
-  P.prune = tk.prune && T.n > TOPK_KC;
+  P.prune = T.n > TOPK_KC;
   std::vector<double> VP;
   TRYC(topk_dst_basis(c, T, P, VP));
   HIPCHK(P.d_VP.ensure(VP.size() * 8));
@@ -1624,7 +1571,6 @@ int topk_plan(als_ctx* c, int src, int k, TopkPlan& P) {
 // ([nc][k], score desc, id asc); rows that fail certification are re-scored exactly and their ids
 // appended to c->last_rescan.  Enqueued on c->st; returns after the rescans are enqueued.
 int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int32_t* d_oid, float* d_osc) {
-  static const TopkKnobs tk;
   Side& S = c->s[P.src];
   Side& T = c->s[1 - P.src];
   const int KP = c->KP, k = P.k;
@@ -1678,7 +1624,6 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int3
   // scan order: rows that stop at similar depths share a workgroup (topk_order); the select writes
   // each row's results back to its own slot
   TopkArgs b = a;
-  b.drain = tk.drain;
   HIPCHK(P.d_okeys.ensure(nc * 8));
   HIPCHK(P.d_order.ensure(nc * 8));
   HIPCHK(P.d_srcs.ensure(nc * 4));
@@ -1692,7 +1637,7 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int3
                     P.d_thr.as<float>(), P.d_thr.as<float>() + nc, sf_tmp, sf_sorted, c->st));
   b.src_rows = P.d_srcs.as<int32_t>();
   b.out_pos = P.d_order.as<uint32_t>();
-  b.thr0 = tk.thr0 ? P.d_thr.as<float>() + nc : nullptr;
+  b.thr0 = P.d_thr.as<float>() + nc;
   b.sfeat = sf_sorted;
   const int rpw = topk_rows_per_workgroup(KP, nc, c->n_cu);
   if (P.prune) {  // per scan workgroup, the chunks its rows can need against the starting thresholds

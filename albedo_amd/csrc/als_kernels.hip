@@ -338,15 +338,9 @@ hipError_t launch_gram(int KP, const float* X, int64_t n, double* slab, int nblk
     gram_partial_kernel<64><<<nblk, 256, 0, s>>>(X, n, per, slab);
     gram_reduce_kernel<64><<<(nt * 256 + 255) / 256, 256, 0, s>>>(slab, nblk, G);
   } else if (KP == 128) {
-    // bf16 MFMA form unless ALBEDO_GRAM_BF=0 (the fp32 16x16x4 form, A/B)
-    static const bool bf = !(getenv("ALBEDO_GRAM_BF") && atoi(getenv("ALBEDO_GRAM_BF")) == 0);
-    if (bf) {
-      gram_bf_kernel<<<nblk, 256, 0, s>>>(X, n, (per + 63) & ~int64_t(63), slab);
-      gram_reduce_nat_kernel<<<(nt * 256 + 255) / 256, 256, 0, s>>>(slab, nblk, G, 128);
-    } else {
-      gram_partial_kernel<128><<<nblk, 256, 0, s>>>(X, n, per, slab);
-      gram_reduce_kernel<128><<<(nt * 256 + 255) / 256, 256, 0, s>>>(slab, nblk, G);
-    }
+    // bf16 MFMA form (three-part split, gram_bf_kernel)
+    gram_bf_kernel<<<nblk, 256, 0, s>>>(X, n, (per + 63) & ~int64_t(63), slab);
+    gram_reduce_nat_kernel<<<(nt * 256 + 255) / 256, 256, 0, s>>>(slab, nblk, G, 128);
   } else if (KP == 256) {
     gram_partial_kernel<256><<<dim3(nblk, gram_waves<256>() / 4), 256, 0, s>>>(X, n, per, slab);
     gram_reduce_kernel<256><<<(nt * 256 + 255) / 256, 256, 0, s>>>(slab, nblk, G);
@@ -640,8 +634,8 @@ hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64
 // Entries with c = 0 (implicit zero ratings) contribute nothing to A or b and are masked out.
 // =============================================================================================
 // LDS floats per wave: D = 16 keeps K and L as packed lower triangles (+ 64: sink); D = 32 / 64 factor
-// in the MFMA accumulators (wave_chol.h) and need its scratch (512 floats + NB L⁻¹ tiles)
-__host__ __device__ constexpr int light_wave_lds(int D) { return D == 16 ? D * (D + 1) / 2 + 64 : 512 + (D / 16) * 256; }
+// in the MFMA accumulators (wave_chol.h) and need its scratch (512 floats)
+__host__ __device__ constexpr int light_wave_lds(int D) { return D == 16 ? D * (D + 1) / 2 + 64 : 512; }
 
 template <int KP, int D>
 constexpr int light_occupancy() { return (D == 16 && KP <= 128) ? 6 : (KP <= 128) ? 4 : 2; }
@@ -2080,9 +2074,9 @@ __global__ __launch_bounds__(Heavy<KP>::NTH) void solve_nnls_kernel(SolveArgs a,
 template <int KP>
 hipError_t launch_nnls_kp(const SolveArgs& a, const float* Gt, hipStream_t s) {
   const size_t lds = NnlsLds<KP>::FLOATS * 4;
-  // KP >= 128: A in registers (nnls_reg_iterate); ALBEDO_NNLS_REG=0 keeps the LDS-streamed loop
+  // KP >= 128: A in registers (nnls_reg_iterate); KP = 64 keeps the LDS-streamed loop
   constexpr bool CAN_REG = KP >= 128;
-  static const bool reg = CAN_REG && !(getenv("ALBEDO_NNLS_REG") && atoi(getenv("ALBEDO_NNLS_REG")) == 0);
+  constexpr bool reg = CAN_REG;
   static const hipError_t attr = allow_lds(solve_nnls_kernel<KP, false>, lds);
   static const hipError_t attr2 = allow_lds(solve_nnls_kernel<KP, true>, lds);
   static const hipError_t attr3 = allow_lds(solve_nnls_kernel<KP, false, CAN_REG>, lds);

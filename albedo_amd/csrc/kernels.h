@@ -168,7 +168,6 @@ struct TopkArgs {
   unsigned long long* scanned;  // += dst chunks scanned by each scan workgroup (or null)
   const uint32_t* out_pos;      // select: results of scan position i go to slot out_pos[i] (or i)
   const float* thr0;            // scan: starting threshold of each src position (topk_order; or null)
-  int drain;                    // debug: drain the VM counter every chunk
 };
 constexpr int TOPK_KC = 64;     // candidates rescored exactly per src row (k <= 64)
 constexpr int TOPK_CAP = 128;   // candidate list capacity per src row (compacted to 64 above TOPK_TRIG)

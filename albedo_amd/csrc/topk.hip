@@ -376,7 +376,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
   for (int64_t c = next_chunk(-1); c < nch; c = next_chunk(c), ++it) {
     // this wave's DMAs of chunk c have landed (in-order VM counter; later list stores only make the
     // wait stricter), then one barrier publishes every wave's part and retires the previous slot
-    if (n_iss - it - 1 >= C::NSTG - 2 && !a.drain) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NVM * (C::NSTG - 2)) : "memory");
+    if (n_iss - it - 1 >= C::NSTG - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NVM * (C::NSTG - 2)) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -987,10 +987,6 @@ hipError_t launch_scan(const TopkArgs& a, hipStream_t s) {
 // that still gives every CU two workgroups, down to G = 2
 int topk_rows_per_workgroup(int KP, int64_t n_src, int n_cu) {
   int gmax = KP <= 128 ? 8 : 4;
-  if (const char* e = std::getenv("ALBEDO_TOPK_GMAX")) {  // experiments: cap the register blocking
-    const int v = std::atoi(e);
-    if (v == 2 || v == 4 || v == 8) gmax = std::min(gmax, v);
-  }
   for (int G = gmax; G > 2; G /= 2)
     if (n_src >= (int64_t)2 * n_cu * 64 * G) return 64 * G;
   return 128;

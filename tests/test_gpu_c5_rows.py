@@ -84,8 +84,7 @@ def test_c5_nnls_rows_match_oracle(gpu_lib):
         with open(os.path.join(OUT, "c5_nnls_rows.json"), "w") as fh:
             json.dump(report, fh)
         print(json.dumps(report))
-        if os.environ.get("ALBEDO_NNLS_BATCH") != "0":  # (A/B runs switch the lockstep kernel off)
-            assert st[0] > 4_000_000  # the lockstep kernel took the low-degree rows
+        assert st[0] > 4_000_000  # the lockstep kernel took the low-degree rows
         for name, e in worst.items():
             assert e <= 1e-3, (name, report)
     finally:

@@ -747,7 +747,6 @@ def test_nnls_lockstep_light_rows(gpu_lib, monkeypatch, k, wgs):
     from albedo_amd.synthetic import SynthSpec, generate
     if wgs:
         monkeypatch.setenv("ALBEDO_NNLS_BATCH_WGS", str(wgs))
-    monkeypatch.delenv("ALBEDO_NNLS_MINSLOTS", raising=False)
     n_users = 330 if k == 256 else 613
     d = generate(SynthSpec(n_users, 90, n_users * 4 + 150, seed=43 + k))
     B = O.make_blocks(d["user"], d["item"], d["rating"])

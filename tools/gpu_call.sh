@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU call of this round: steps given as arguments are run in order, each under its own time
 # limit; the call stops at the first failing step.  usage: tools/gpu_call.sh <step> [<step> ...]
-#   bounds_c2 | bounds_c4 | tests_quick | tests_scale | tests_all | smoke | bench_c4 | bench_c2 | bench_c5
+#   bounds_c2 | bounds_c4 | tests_* | smoke | bench_c4 | bench_c2 | bench_c5 | prof_* | trace_* | probes
 set -e
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
@@ -24,22 +24,18 @@ for s in "$@"; do
     prof_c2) timeout -k 10 600 tools/prof.sh c2 r03 16384 > gpurun_out/prof_c2.log 2>&1 ;;
     trace_c4) mkdir -p gpurun_out/trace_c4 && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_c4 -o run -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu --topk-users 16384 > gpurun_out/trace_c4/bench.json 2> gpurun_out/trace_c4/bench.err ;;
     trace_topk) mkdir -p gpurun_out/trace_topk && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_topk -o run -- python3 -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/trace_topk/bench.json 2> gpurun_out/trace_topk/bench.err ;;
-    ab_c4) for v in 0 1; do ALBEDO_LIGHT16=$v timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu --topk-users 0 > gpurun_out/ab_c4_$v.json 2> gpurun_out/ab_c4_$v.err || exit 1; done ;;
     tests_solve) timeout -k 10 700 $PYT tests/test_gpu_parity.py tests/test_gpu_heavy_tail.py tests/test_gpu_scale.py -k "half_sweep or golden or facade or albedo_protocol or column_scaling or positive_definite or heavy or c4_scale_rows or c2_scale" > gpurun_out/tests_solve.log 2>&1 ;;
     tests_nnls) timeout -k 10 700 $PYT tests/test_gpu_parity.py tests/test_gpu_heavy_tail.py tests/test_gpu_c5_rows.py -k "nnls or c5" > gpurun_out/tests_nnls.log 2>&1 ;;
-    ab_c5) for v in 0 1; do ALBEDO_NNLS_REG=$v timeout -k 10 400 python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/ab_c5_$v.json 2> gpurun_out/ab_c5_$v.err || exit 1; done ;;
-    probe_bo) ALBEDO_ALS_LIB=tools/probe/libwave_buildonly.so timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/probe_bo.json 2> gpurun_out/probe_bo.err || true ;;
-    c5_slots16) ALBEDO_NNLS_MINSLOTS=16 timeout -k 10 400 python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/c5_slots16.json 2> gpurun_out/c5_slots16.err ;;
     nnlstime) timeout -k 5 60 tools/probe/nnlstime 256 100000 2048 200 > gpurun_out/nnlstime.txt 2>&1 ;;
-    ab_rot) for v in 0 1; do ALBEDO_ROTATE_BF=$v timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu --topk-users 0 > gpurun_out/ab_rot_$v.json 2> gpurun_out/ab_rot_$v.err || exit 1; done ;;
     tests_gram) timeout -k 10 300 $PYT tests/test_gpu_heavy_tail.py -k "gram" > gpurun_out/tests_gram.log 2>&1 ;;
-    grid) bash tools/grid_check.sh ;;
     trace_c5) mkdir -p gpurun_out/trace_c5 && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_c5 -o run -- python3 -u bench.py --config c5 --steps 1 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/trace_c5/bench.json 2> gpurun_out/trace_c5/bench.err ;;
     tests_mr) timeout -k 10 900 $PYT tests/test_multi_rank.py > gpurun_out/tests_mr.log 2>&1 ;;
     wavetime) (cd tools/probe && timeout -k 5 120 ./wavetime 20000000 80,160,320,640,1280,4096 200000000 && timeout -k 5 120 ./wavetime_bo 20000000 80,160,320,640,1280,4096 200000000) > gpurun_out/wavetime.txt 2>&1 ;;
+    wavetime1) (cd tools/probe && timeout -k 5 120 ./wavetime 20000000 80,160,320,640,1280,4096 200000000) > gpurun_out/wavetime1.txt 2>&1 ;;
     c1p) timeout -k 10 900 python -u tools/c1p_job.py --out gpurun_out/c1p_job.json > gpurun_out/c1p_job.log 2>&1 ;;
     tests_eig) timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "device_eigensolver or half_sweep_ranks" > gpurun_out/tests_eig.log 2>&1 ;;
     bench_c4q) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 > gpurun_out/bench_c4q.json 2> gpurun_out/bench_c4q.err ;;
+    factortime) (cd tools/probe && timeout -k 5 120 ./factortime 1000000) > gpurun_out/factortime.txt 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

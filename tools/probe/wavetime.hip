@@ -71,7 +71,7 @@ int main(int argc, char** argv) {
     SolveArgs a{};
     a.Z = Z; a.Zhl = Zhl; a.zero_row = nsrc; a.wsc = 1.f; a.inv_sw = 1.f;
     a.ptr = ptr; a.col = col; a.val = val; a.rows = rows; a.n_rows = nrows; a.lam = lam; a.X = X;
-    a.kreal = KP; a.implicit = 1; a.alpha = 40.f; a.reg = 0.5f; a.err = err; a.colscale = cs;
+    a.kreal = KP; a.implicit = 1; a.alpha = 40.f; a.reg = 0.5f; a.err = err; a.colscale = cs; a.n_cu = 256;
     CK(launch_solve_wave(KP, a, 0));
     CK(hipDeviceSynchronize());
     const int reps = 3;
