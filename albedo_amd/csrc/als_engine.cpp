@@ -173,6 +173,10 @@ struct als_ctx {
   // top-k counters, cumulative: [0] rows through the MFMA scan, [1] rows re-scored by the exact scan
   // (certification misses), [2] dst chunks scanned, [3] dst chunks a full scan would take
   int64_t topk_stats[4] = {0, 0, 0, 0};
+  // top-k device time, cumulative (ms, HIP events on st): [0] order + mask, [1] MFMA scan, [2] select,
+  // [3] exact rescans; [4] scan flops (2·KP per src x dst pair the scan's waves scored)
+  double topk_ms[5] = {0, 0, 0, 0, 0};
+  hipEvent_t evt[5] = {};
   std::vector<int32_t> last_rescan;  // src ids the last als_recommend sent to the exact rescan
   int split_len = 0;             // ratings per split-K chunk (0: no split)
   int slab_blocks = 0;
@@ -618,6 +622,17 @@ int spark_init(als_ctx* c) {
   return ALS_OK;
 }
 
+// the solve paths named by the bits of a not-positive-definite flag word (kernels.h ALBEDO_EF_*)
+std::string err_paths(int err) {
+  std::string r;
+  const std::pair<int, const char*> names[] = {{ALBEDO_EF_LIGHT16, "light16"}, {ALBEDO_EF_LIGHT_REG, "light-d16"},
+                                               {ALBEDO_EF_LIGHT_ACC, "light"}, {ALBEDO_EF_WAVE, "wave"},
+                                               {ALBEDO_EF_HEAVY, "heavy"}};
+  for (const auto& n : names)
+    if (err & n.first) r += std::string(r.empty() ? ": " : ",") + n.second;
+  return r;
+}
+
 float event_ms(hipEvent_t a, hipEvent_t b) {
   float ms = 0.f;
   (void)hipEventElapsedTime(&ms, a, b);
@@ -979,7 +994,7 @@ int half_sweep(als_ctx* c, int t) {
     return fail(ALS_E_NOT_POSITIVE_DEFINITE,
                 "LAPACK.dppsv-equivalent Cholesky met a non-positive pivot because A is not positive "
                 "definite. Is A derived from a singular matrix (e.g. collinear column values)? (flags " +
-                    std::to_string(err) + ", " + std::to_string(sweeps) + " eigensolver sweeps)");
+                    std::to_string(err) + err_paths(err) + ", " + std::to_string(sweeps) + " eigensolver sweeps)");
   T.has_factors = true;
   T.orig_valid = false;
   T.full_valid = multi;  // gathered behind the solve (st2); the next half waits for it
@@ -1089,6 +1104,7 @@ static int ctx_common(const als_params* p, als_ctx** out) {
     return fail(ALS_E_HIP, "failed to create a HIP stream");
   }
   for (auto& e : c->ev) (void)hipEventCreate(&e);
+  for (auto& e : c->evt) (void)hipEventCreate(&e);
   for (auto& e : c->evc) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   if (hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) != hipSuccess) {
     delete c;
@@ -1217,6 +1233,8 @@ static void destroy_now(als_ctx* c) {
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->evc)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->evt)
     if (e) (void)hipEventDestroy(e);
   if (c->st2) (void)hipStreamDestroy(c->st2);
   if (c->st) (void)hipStreamDestroy(c->st);
@@ -1624,6 +1642,7 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int3
   // scan order: rows that stop at similar depths share a workgroup (topk_order); the select writes
   // each row's results back to its own slot
   TopkArgs b = a;
+  HIPCHK(hipEventRecord(c->evt[0], c->st));
   HIPCHK(P.d_okeys.ensure(nc * 8));
   HIPCHK(P.d_order.ensure(nc * 8));
   HIPCHK(P.d_srcs.ensure(nc * 4));
@@ -1647,7 +1666,11 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int3
     b.mask = P.d_mask.as<uint32_t>();
     HIPCHK(launch_topk_mask(b, rpw, P.d_supf.as<float>(), P.n_super, P.d_mask.as<uint32_t>(), c->st));
   }
+  HIPCHK(hipEventRecord(c->evt[1], c->st));
   HIPCHK(launch_topk(KP, b, c->n_cu, c->st));
+  HIPCHK(hipEventRecord(c->evt[2], c->st));
+  HIPCHK(launch_topk_select(KP, b, c->st));
+  HIPCHK(hipEventRecord(c->evt[3], c->st));
   std::vector<int32_t> need(nc);
   unsigned long long scanned = 0;
   HIPCHK(hipMemcpyAsync(need.data(), P.d_need.p, nc * 4, hipMemcpyDeviceToHost, c->st));
@@ -1663,11 +1686,18 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int3
   c->topk_stats[1] += (int64_t)flagged.size();
   c->topk_stats[2] += (int64_t)scanned;
   c->topk_stats[3] += (nc + rpw - 1) / rpw * 4 * P.n_chunks * P.CH;  // dst rows x waves
+  c->topk_ms[0] += event_ms(c->evt[0], c->evt[1]);
+  c->topk_ms[1] += event_ms(c->evt[1], c->evt[2]);
+  c->topk_ms[2] += event_ms(c->evt[2], c->evt[3]);
+  c->topk_ms[4] += (double)scanned * (rpw / 4) * 2.0 * KP;  // per wave: rpw / 4 src rows x each dst row
   if (!flagged.empty()) {
     HIPCHK(P.d_flag.ensure(flagged.size() * 4));
     HIPCHK(hipMemcpyAsync(P.d_flag.p, flagged.data(), flagged.size() * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipEventRecord(c->evt[0], c->st));
     HIPCHK(launch_topk_exact(KP, a, P.d_flag.as<int32_t>(), (int64_t)flagged.size(), c->st));
+    HIPCHK(hipEventRecord(c->evt[4], c->st));
     HIPCHK(hipStreamSynchronize(c->st));  // flagged (host) must outlive the async copy
+    c->topk_ms[3] += event_ms(c->evt[0], c->evt[4]);
   }
   return ALS_OK;
 }
@@ -1936,6 +1966,12 @@ int als_solver_stats(const als_ctx* c, int dst_side, int64_t* out4) {
 int als_topk_stats(const als_ctx* c, int64_t* out4) {
   if (!c || !out4) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
   for (int i = 0; i < 4; ++i) out4[i] = c->topk_stats[i];
+  return ALS_OK;
+}
+
+int als_topk_timing(const als_ctx* c, double* out5) {
+  if (!c || !out5) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  for (int i = 0; i < 5; ++i) out5[i] = c->topk_ms[i];
   return ALS_OK;
 }
 

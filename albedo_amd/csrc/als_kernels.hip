@@ -634,8 +634,8 @@ hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64
 // Entries with c = 0 (implicit zero ratings) contribute nothing to A or b and are masked out.
 // =============================================================================================
 // LDS floats per wave: D = 16 keeps K and L as packed lower triangles (+ 64: sink); D = 32 / 64 factor
-// in the MFMA accumulators (wave_chol.h) and need its scratch (512 floats)
-__host__ __device__ constexpr int light_wave_lds(int D) { return D == 16 ? D * (D + 1) / 2 + 64 : 512; }
+// in the MFMA accumulators (wave_chol.h) and need its scratch (WCHOL_SCR floats + NB L⁻¹ tiles)
+__host__ __device__ constexpr int light_wave_lds(int D) { return D == 16 ? D * (D + 1) / 2 + 64 : WCHOL_SCR + (D / 16) * 256; }
 
 template <int KP, int D>
 constexpr int light_occupancy() { return (D == 16 && KP <= 128) ? 6 : (KP <= 128) ? 4 : 2; }
@@ -803,7 +803,7 @@ __device__ __forceinline__ void light_row(const SolveArgs& a, int j, int d, floa
       const float yc = bc16<c>(y * dg);
       y = (me > c) ? fmaf(-kr[c], yc, y) : ((me == c) ? yc : y);
     });
-    if (notpd && lane == 0) atomicOr(a.err, 2);
+    if (notpd && lane == 0) atomicOr(a.err, 2 | ALBEDO_EF_LIGHT_REG);
     // transpose L through LDS: lane i gets column i (lt[m] = L[m][i])
     WAVE_LDS_SYNC();
     if (lane < D) {
@@ -836,7 +836,7 @@ __device__ __forceinline__ void light_row(const SolveArgs& a, int j, int d, floa
     });
     float xs[NB];
     const bool notpd = wave_chol_solve<NB>(acc, bacc, Ks, xs);
-    if (notpd && lane == 0) atomicOr(a.err, 2);
+    if (notpd && lane == 0) atomicOr(a.err, 2 | ALBEDO_EF_LIGHT_ACC);
     y = 0.f;  // lane 16A + i holds v[16A + i] = xs[A] (its own slot A = g)
 #pragma unroll
     for (int A = 0; A < NB; ++A) y = g == A ? xs[A] : y;
@@ -1335,7 +1335,7 @@ __global__ __launch_bounds__(Heavy<KP>::NTH, 4) void solve_heavy_kernel(SolveArg
       for (int c = 0; c < 16; ++c) t[c * 16 + i16] = c <= i16 ? rr[c] : 0.f;
       sdiag[16 * jb + i16] = dg;
     }
-    if (np && lane == 0) s_flag[1] = 2;
+    if (np && lane == 0) s_flag[1] = 2 | ALBEDO_EF_HEAVY;
   };
   // C(I,M) -= L(I,jb) L(M,jb)ᵀ on MFMA (packed lower 16x17 tiles)
   auto tile_update = [&](int jb, int I, int M) {

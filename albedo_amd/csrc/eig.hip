@@ -7,7 +7,7 @@
 // coordinates, so  W = B_sᵀ·B_t  nearly diagonalises the new Gram G (the factors change little from
 // one sweep to the next):  M = Wᵀ G W  is swept by a cyclic parallel Jacobi in fp64 (one workgroup,
 // M in LDS, the 64 disjoint pairs of a round-robin round rotated at once, V = W·J accumulated in
-// global memory) until the off-diagonal mass is below 1e-30 of the diagonal's.  Then P = V, Λ = diag,
+// global memory) until the off-diagonal mass is below 1e-28 of the diagonal's (JAC_TOL).  Then P = V, Λ = diag,
 // and the new dst basis B_t = B_s·P.  From a warm start the sweep count is small (2-4); from the
 // identity (first half-sweep) it is the usual 6-10.  Deterministic: fixed pairing, fixed order.
 #include <hip/hip_runtime.h>
@@ -37,6 +37,12 @@ __global__ __launch_bounds__(256) void dgemm_kp_kernel(const double* __restrict_
 
 constexpr int JAC_THREADS = 1024;
 constexpr int JAC_MAX_SWEEPS = 30;
+// Convergence: off-diagonal mass <= 1e-28 of the diagonal's (off-diagonal norm 1e-14 of the diagonal's,
+// about fp64 rounding at k <= 256: a backward error of the order of a Householder + QL solve).  The
+// small eigenpairs need it: at 1e-9 the directions of eigenvalues near 1e-9·‖G‖ keep components of the
+// large ones, and the per-row systems built on them (D = Λ + λn, push-through S = Z D⁻¹ Zᵀ) lose
+// positive definiteness in fp32.  Below 1e-20, a sweep that does not halve the mass (the rounding floor) also stops.
+constexpr double JAC_TOL = 1e-28;
 
 // round r of the round-robin over n (even) players: pair i = (a, b); player n-1 is fixed
 __device__ __forceinline__ void rr_pair(int r, int i, int n, int& a, int& b) {
@@ -63,6 +69,7 @@ __global__ __launch_bounds__(JAC_THREADS) void jacobi_kernel(double* __restrict_
   __shared__ int pq[2 * 128];     // p, q
   __shared__ double red[JAC_THREADS / 64][2];
   __shared__ int done;
+  double prev_off = INFINITY;  // thread 0's
   const int ld = LDSM ? k + 1 : KP;  // LDS: padded row stride (column walks spread over the banks)
   double* M = LDSM ? sm : Mg;
   const int tid = threadIdx.x;
@@ -96,7 +103,8 @@ __global__ __launch_bounds__(JAC_THREADS) void jacobi_kernel(double* __restrict_
         so += red[i][0];
         sd += red[i][1];
       }
-      done = !(so > 1e-18 * sd);  // off-diagonal norm <= 1e-9 of the diagonal's (P is used in fp32)
+      done = !(so > JAC_TOL * sd) || (!(so > 1e-20 * sd) && !(so < 0.5 * prev_off));  // or at the rounding floor
+      prev_off = so;
     }
     __syncthreads();
     if (done) break;
@@ -171,6 +179,7 @@ __global__ __launch_bounds__(JAC_THREADS) void jacobi_lds_kernel(const double* _
   __shared__ int pq[2 * 64];
   __shared__ double red[JAC_THREADS / 64][2];
   __shared__ int done;
+  double prev_off = INFINITY;  // thread 0's
   const int ld = k + 1;           // M row stride (column walks spread over the banks)
   const int nc = KP / JAC_WG;     // VT columns of this workgroup
   const int c0 = blockIdx.x * nc;
@@ -206,8 +215,8 @@ __global__ __launch_bounds__(JAC_THREADS) void jacobi_lds_kernel(const double* _
         so += red[i][0];
         sd += red[i][1];
       }
-      // off-diagonal norm <= 1e-9 of the diagonal's: P is used in fp32 (its rounding is 6e-8)
-      done = !(so > 1e-18 * sd);
+      done = !(so > JAC_TOL * sd) || (!(so > 1e-20 * sd) && !(so < 0.5 * prev_off));  // or at the rounding floor
+      prev_off = so;
     }
     __syncthreads();
     if (done) break;

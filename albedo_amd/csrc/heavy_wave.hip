@@ -22,7 +22,6 @@
 // Against the 4-wave workgroup kernel this trades 4 waves x 39 KB of LDS per row for one wave and
 // 16.5 KB: twice the rows in flight per CU, and no workgroup barriers in the factorisation.
 #include <hip/hip_runtime.h>
-#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include "device_common.h"
@@ -55,9 +54,9 @@ struct WaveRow {
   static constexpr int STAGE = SPS * RB + 64 * (SPS / 8 - 1);  // + 64 B per 8-rating group (banks)
   static constexpr int WAVES = 4;                        // rows per workgroup (independent waves)
   static constexpr int LDS_WAVE = (STAGE + 255) & ~255;
-  static constexpr int SCR = 512 * 4;                    // per-wave scratch of b' and the factorisation
-  static constexpr int LDS = WAVES * (LDS_WAVE + SCR) + 2 * KP * 4;  // + column scales and inverses
+  static constexpr int LDS = WAVES * LDS_WAVE + 2 * KP * 4;  // + column scales and inverses
   static_assert(RPI * RB == 1024 && 8 % RPI == 0, "DMA pieces never cross an 8-rating group");
+  static_assert(LDS_WAVE >= 4 * WCHOL_SCR + NQ * 1024, "the stage doubles as the factor's scratch + L⁻¹ store");
 };
 
 // LDS byte offset of (rating r of the stage, column c).  Lane i + 16q reads ratings 8q..8q+7 of
@@ -77,33 +76,16 @@ __device__ __forceinline__ f16x4v tr_read(const char* p) {
   return __builtin_bit_cast(f16x4v, v);
 }
 
-// A wave's gather pipeline, carried from row to row by the persistent solve kernel: while stage s of a
-// row is on the matrix cores, stage s + 1's rows are in flight into the LDS stage and stage s + 2's
-// (col, val) into registers.  At a row's last stage the pipeline runs on into the NEXT row (pn, dn):
-// its stage 0 is gathered while this row is scaled and factored, so the next build starts on data
-// that has landed.  primed: stage 0 of the row about to be built is issued (c_cur, r_cur) and stage
-// 1's indices (if it has one) are loaded; nxt0: c_nxt / r_nxt hold the next row's stage-0 indices.
-struct WaveFeed {
-  int c_cur = 0, c_nxt = 0;
-  float r_cur = 0.f, r_nxt = 0.f;
-  bool primed = false, nxt0 = false;
-  int64_t pn = 0;  // next row: first rating, count (0: none)
-  int dn = 0;
-};
-
 // The build of one row's (or split-K chunk's) normal equation by one wave: ratings p0 .. p0+d-1 of
 // the CSR, gathered 32 per stage into this wave's LDS stage st.  On return acc holds the NT upper
 // tiles of Σ c·(cs z)(cs z)ᵀ (still column-scaled), bacc[A] (lane i + 16q) b'[16A + i] unscaled;
-// returns the number of positive ratings.  scr: the wave's scratch (256 floats, for b').
-// lane: threadIdx.x & 63 (the persistent kernel passes a value laundered per row, so that no lane-
-// derived address is hoisted out of its row loop and kept live across the factorisation)
+// returns the number of positive ratings.
 template <int KP, bool IMPLICIT, bool PRE>
-__device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d, char* st, float* scr,
-                                          const float* s_cs, f32x4 (&acc)[WaveRow<KP>::NT],
-                                          float (&bacc)[WaveRow<KP>::NQ], WaveFeed& f, const int lane) {
+__device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d, char* st, const float* s_cs,
+                                          f32x4 (&acc)[WaveRow<KP>::NT], float (&bacc)[WaveRow<KP>::NQ]) {
   using W = WaveRow<KP>;
   constexpr int NQ = W::NQ, NT = W::NT;
-  const int q = lane >> 4, i16 = lane & 15;
+  const int lane = threadIdx.x & 63, q = lane >> 4, i16 = lane & 15;
   const int nst = (d + W::SPS - 1) / W::SPS;
 
 #pragma unroll
@@ -114,19 +96,17 @@ __device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d,
   for (int e = 0; e < CPL; ++e) bpart[e] = 0.f;
   int npos = 0;
 
-  // (col, val) of stage s of the row (pb, db): lane l holds rating 32 s + (l & 31), clamped to the
-  // row (zero weight)
-  auto iload_row = [&](int64_t pb, int db, int s, int& c_out, float& r_out) {
+  // (col, val) of stage s: lane l holds rating 32 s + (l & 31), clamped to the row (zero weight)
+  auto iload = [&](int s, int& c_out, float& r_out) {
     const int e = W::SPS * s + (lane & 31);
-    const int64_t pe = pb + (e < db ? e : db - 1);
+    const int64_t pe = p0 + (e < d ? e : d - 1);
     c_out = a.col[pe];
     r_out = a.val[pe];
     if constexpr (PRE) {  // past the row end: the zero row (its products vanish in A' and b')
-      c_out = e < db ? c_out : (int)a.zero_row;
-      r_out = e < db ? r_out : 0.f;
+      c_out = e < d ? c_out : (int)a.zero_row;
+      r_out = e < d ? r_out : 0.f;
     }
   };
-  auto iload = [&](int s, int& c_out, float& r_out) { iload_row(p0, d, s, c_out, r_out); };
   // gather of one stage: piece u holds ratings RPI·u .. RPI·u + RPI-1, lane l the 16 B at
   // 4·(l % LPR) of rating RPI·u + l / LPR; the rating's src row is wave-uniform (readlane)
   auto dma = [&](int cidx) {
@@ -152,31 +132,20 @@ __device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d,
     });
   };
 
-  int& c_cur = f.c_cur;
-  int& c_nxt = f.c_nxt;
-  float& r_cur = f.r_cur;
-  float& r_nxt = f.r_nxt;
-  // the stage's fragments are in registers: refill the stage with s + 1 and fetch the indices of the
-  // stage after that (past the row's end: the next row's stage 0)
+  int c_cur = 0, c_nxt = 0;
+  float r_cur = 0.f, r_nxt = 0.f;
+  // the stage's fragments are in registers: refill the stage with s + 1, fetch the indices of s + 2
   auto next_stage = [&](int s) {
-    if (s + 1 < nst) {
-      dma(c_nxt);
-      c_cur = c_nxt;
-      r_cur = r_nxt;
-      if (s + 2 < nst) iload(s + 2, c_nxt, r_nxt);
-      else if (f.dn > 0) {
-        iload_row(f.pn, f.dn, 0, c_nxt, r_nxt);
-        f.nxt0 = true;
-      }
-    }
+    dma(c_nxt);
+    c_cur = c_nxt;
+    r_cur = r_nxt;
+    if (s + 2 < nst) iload(s + 2, c_nxt, r_nxt);
   };
-  if (nst > 0 && !f.primed) {
+  if (nst > 0) {
     iload(0, c_cur, r_cur);
     dma(c_cur);
     if (nst > 1) iload(1, c_nxt, r_nxt);
   }
-  f.primed = false;
-  f.nxt0 = false;
   f32x4 bt = zero4();  // PRE: b' of every block in one tile (column 2A: w hi, 2A + 1: w lo)
   for (int s = 0; s < nst; ++s) {
     const bool in = W::SPS * s + (lane & 31) < d;
@@ -225,7 +194,7 @@ __device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d,
         });
       }
       WAVE_LDS_SYNC();
-      next_stage(s);
+      if (s + 1 < nst) next_stage(s);
       __builtin_amdgcn_sched_barrier(0);
       static_for<0, NQ>([&](auto AA) {
         constexpr int A = decltype(AA)::value;
@@ -276,7 +245,7 @@ __device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d,
         }
       }
       WAVE_LDS_SYNC();
-      next_stage(s);
+      if (s + 1 < nst) next_stage(s);
       __builtin_amdgcn_sched_barrier(0);
       static_for<0, NQ>([&](auto AA) {
         static_for<decltype(AA)::value, NQ>([&](auto BB) {
@@ -287,20 +256,10 @@ __device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d,
     }
   }
 
-  // the next row's stage 0 into the stage, now free (issued after the last MFMAs: no fragment is live)
-  if (f.dn > 0) {
-    if (!f.nxt0) iload_row(f.pn, f.dn, 0, c_nxt, r_nxt);
-    dma(c_nxt);
-    c_cur = c_nxt;
-    r_cur = r_nxt;
-    if (f.dn > W::SPS) iload_row(f.pn, f.dn, 1, c_nxt, r_nxt);
-    f.primed = true;
-  }
   __builtin_amdgcn_sched_barrier(0);  // keep the factor's loads out of the build loop
   // ---- b' complete (sum over the four rating groups), tiles unscaled, diagonal Λ + λn ----------
-  // b' to the factor's layout (lane i + 16q holds b'[16A + i] for every block A) through LDS (the
-  // scratch: the stage may already be receiving the next row)
-  float* bsc = scr;
+  // b' to the factor's layout (lane i + 16q holds b'[16A + i] for every block A) through LDS
+  float* bsc = reinterpret_cast<float*>(st);
   if constexpr (PRE) {  // bt: lane j + 16q holds column j (block j >> 1, w hi / lo), rows 4q .. 4q+3
 #pragma unroll
     for (int r = 0; r < 4; ++r) bsc[16 * i16 + 4 * q + r] = bt[r];
@@ -321,124 +280,98 @@ __device__ __forceinline__ int wave_build(const SolveArgs& a, int64_t p0, int d,
   return npos;
 }
 
-// Persistent: the grid holds as many workgroups as fit at once and wave w takes rows w, w + W, ...
-// (W = every wave of the grid; the rows are sorted by degree, so every wave gets the same mix).  The
-// next row's descriptor is read at the start of a row and its first stage is gathered while this row
-// is scaled and factored (WaveFeed).
 template <int KP, bool IMPLICIT, bool PRE>
 __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
   using W = WaveRow<KP>;
   constexpr int NQ = W::NQ, NT = W::NT;
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int lane = threadIdx.x & 63, q = lane >> 4, i16 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // scalar: LDS-DMA bases in SGPRs
-  float* s_cs = reinterpret_cast<float*>(lds + W::WAVES * (W::LDS_WAVE + W::SCR));  // [KP] scales, [KP] inverses
+  float* s_cs = reinterpret_cast<float*>(lds + W::WAVES * W::LDS_WAVE);  // [KP] scales, [KP] inverses
   for (int e = threadIdx.x; e < 2 * KP; e += 256) s_cs[e] = a.colscale[e];
-  __syncthreads();  // the only workgroup barrier: every wave below is on its own rows
-  char* st = lds + wave * W::LDS_WAVE;
-  float* scr = reinterpret_cast<float*>(lds + W::WAVES * W::LDS_WAVE + wave * W::SCR);
-  const int64_t wstep = (int64_t)gridDim.x * W::WAVES;
-  int64_t ridx = (int64_t)blockIdx.x * W::WAVES + wave;
+  __syncthreads();  // the only workgroup barrier: every wave below is on its own row
+  const int64_t ridx = (int64_t)blockIdx.x * W::WAVES + wave;
   if (ridx >= a.n_rows) return;
-  int j = a.rows[ridx];
-  int64_t p0 = a.ptr[j];
-  int d = (int)(a.ptr[j + 1] - p0);
-  WaveFeed f;
-  for (; ridx < a.n_rows; ridx += wstep) {
-    const int64_t nidx = ridx + wstep;
-    int jn = 0;
-    f.dn = 0;
-    if (nidx < a.n_rows) {
-      jn = a.rows[nidx];
-      f.pn = a.ptr[jn];
-      f.dn = (int)(a.ptr[jn + 1] - f.pn);
-    }
-    // loop-invariant loads (column scales, eigenvalues) are re-read per row rather than hoisted out of
-    // the row loop, where they would stay live across the factorisation
-    const float* s_csr = s_cs;
-    const float* lamr = a.lam;
-    int lane = threadIdx.x & 63;
-    asm volatile("" : "+s"(s_csr), "+s"(lamr), "+v"(lane));
-    const int q = lane >> 4, i16 = lane & 15;
-    f32x4 acc[NT];
-    float bacc[NQ];
-    WAVE_STAMP(ridx, 0);
-#ifdef WAVE_PROBE_FACTOR_ONLY  // probes only: a synthetic SPD system instead of the build
-    static_for<0, NT>([&](auto T_) { acc[decltype(T_)::value] = f32x4{1e-3f, -2e-3f, 3e-3f, 1e-3f}; });
-    static_for<0, NQ>([&](auto A_) {
-      constexpr int A = decltype(A_)::value;
+  char* st = lds + wave * W::LDS_WAVE;
+  const int j = a.rows[ridx];
+  const int64_t p0 = a.ptr[j];
+  const int d = (int)(a.ptr[j + 1] - p0);
+  f32x4 acc[NT];
+  float bacc[NQ];
+  WAVE_STAMP(ridx, 0);
+#ifdef WAVE_PROBE_FACTOR_ONLY  // probes only (tools/probe/factortime.hip): a synthetic SPD system
+  static_for<0, NT>([&](auto T_) { acc[decltype(T_)::value] = f32x4{1e-3f, -2e-3f, 3e-3f, 1e-3f}; });
+  static_for<0, NQ>([&](auto A_) {
+    constexpr int A = decltype(A_)::value;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[tix(A, A, NQ)][r] = (4 * q + r == i16) ? 100.f + i16 : 1e-3f;
-      bacc[A] = 1.f;
-    });
-    const int npos = d;
+    for (int r = 0; r < 4; ++r) acc[tix(A, A, NQ)][r] = (4 * q + r == i16) ? 100.f + i16 : 1e-3f;
+    bacc[A] = 1.f;
+  });
+  const int npos = d;
 #else
-    const int npos = wave_build<KP, IMPLICIT, PRE>(a, p0, d, st, scr, s_csr, acc, bacc, f, lane);
+  const int npos = wave_build<KP, IMPLICIT, PRE>(a, p0, d, st, s_cs, acc, bacc);
 #endif
-    WAVE_STAMP(ridx, 1);
-    const float lamn = a.reg * (float)(IMPLICIT ? npos : d);
-    const float* isc = s_csr + KP;
-    // The system is scaled by s2 = 4^e (exact) so that its largest diagonal entry stays below 2^28:
-    // every Cholesky entry |U_ij| <= sqrt(A_jj) is then below 2^14, the range the split-fp16 trailing
-    // updates of wave_chol_solve<NQ, true> need.  x is unchanged ((s2·A') x = s2·b').
-    float dmax = 0.f;
-    static_for<0, NQ>([&](auto AA) {
-      constexpr int A = decltype(AA)::value, t = tix(A, A, NQ);
-      const int c = 16 * A + i16;
-      const float ic = isc[c];
-      float dv = 0.f;
+  WAVE_STAMP(ridx, 1);
+  const float lamn = a.reg * (float)(IMPLICIT ? npos : d);
+  const float* isc = s_cs + KP;
+  // The system is scaled by s2 = 4^e (exact) so that its largest diagonal entry stays below 2^28:
+  // every Cholesky entry |U_ij| <= sqrt(A_jj) is then below 2^14, the range the split-fp16 trailing
+  // updates of wave_chol_solve<NQ, true> need.  x is unchanged ((s2·A') x = s2·b').
+  float dmax = 0.f;
+  static_for<0, NQ>([&](auto AA) {
+    constexpr int A = decltype(AA)::value, t = tix(A, A, NQ);
+    const int c = 16 * A + i16;
+    const float ic = isc[c];
+    float dv = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dv = (4 * q + r == i16) ? acc[t][r] : dv;
-      const float dadd = c < a.kreal ? lamr[c] + lamn : 1.0f;
-      dmax = fmaxf(dmax, fabsf(dv * (ic * ic) + dadd));
+    for (int r = 0; r < 4; ++r) dv = (4 * q + r == i16) ? acc[t][r] : dv;
+    const float dadd = c < a.kreal ? a.lam[c] + lamn : 1.0f;
+    dmax = fmaxf(dmax, fabsf(dv * (ic * ic) + dadd));
+  });
+  for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o));
+  int ex = 0;
+  frexpf(dmax, &ex);  // dmax < 2^ex
+  int e2 = (28 - ex) >> 1;
+  e2 = e2 > 60 ? 60 : (e2 < -60 ? -60 : e2);
+  const float s2 = ldexpf(1.f, 2 * e2);
+  static_for<0, NQ>([&](auto AA) {
+    constexpr int A = decltype(AA)::value;
+    const f32x4 ir = ld4(isc + 16 * A + 4 * q) * s2;
+    bacc[A] *= s2;
+    static_for<A, NQ>([&](auto BB) {
+      constexpr int B = decltype(BB)::value, t = tix(A, B, NQ);
+      const float ic = isc[16 * B + i16];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[t][r] *= ir[r] * ic;
+      if constexpr (A == B) {
+        const int c = 16 * A + i16;
+        const float dadd = (c < a.kreal ? a.lam[c] + lamn : 1.0f) * s2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * q + r == i16) acc[t][r] += dadd;
+      }
     });
-    dmax = wave_max_dpp(dmax);
-    int ex = 0;
-    frexpf(dmax, &ex);  // dmax < 2^ex
-    int e2 = (28 - ex) >> 1;
-    e2 = e2 > 60 ? 60 : (e2 < -60 ? -60 : e2);
-    const float s2 = ldexpf(1.f, 2 * e2);
-    static_for<0, NQ>([&](auto AA) {
-      constexpr int A = decltype(AA)::value;
-      const f32x4 ir = ld4(isc + 16 * A + 4 * q) * s2;
-      bacc[A] *= s2;
-      static_for<A, NQ>([&](auto BB) {
-        constexpr int B = decltype(BB)::value, t = tix(A, B, NQ);
-        const float ic = isc[16 * B + i16];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[t][r] *= ir[r] * ic;
-        if constexpr (A == B) {
-          const int c = 16 * A + i16;
-          const float dadd = (c < a.kreal ? lamr[c] + lamn : 1.0f) * s2;
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (4 * q + r == i16) acc[t][r] += dadd;
-        }
-      });
-    });
+  });
 
 #ifdef WAVE_PROBE_BUILD_ONLY
-    if (q == 0) for (int A = 0; A < NQ; ++A) a.X[(int64_t)j * KP + 16 * A + i16] = bacc[A] + acc[tix(A, A, NQ)][0];
-#else
-    // ---- blocked Cholesky A' = UᵀU on the tiles, RHS alongside (wave_chol.h) -----------------------
-    float xs[NQ];
-    const bool notpd = wave_chol_solve<NQ, true>(acc, bacc, scr, xs, lane);
-    WAVE_STAMP(ridx, 2);
-    bool nonfinite = false;
-#pragma unroll
-    for (int A = 0; A < NQ; ++A) {
-      const int c = 16 * A + i16;
-      const float v = c < a.kreal ? xs[A] : 0.f;
-      nonfinite |= !isfinite(v);
-      if (q == 0) a.X[(int64_t)j * KP + c] = v;
-    }
-    WAVE_STAMP(ridx, 3);
-    const bool bad = notpd || __any(nonfinite);  // wave-uniform
-    if (lane == 0 && bad) atomicOr(a.err, 2);
+  if (q == 0) for (int A = 0; A < NQ; ++A) a.X[(int64_t)j * KP + 16 * A + i16] = bacc[A] + acc[tix(A, A, NQ)][0];
+  return;
 #endif
-    j = jn;
-    p0 = f.pn;
-    d = f.dn;
+  // ---- blocked Cholesky A' = UᵀU on the tiles, RHS alongside (wave_chol.h) -----------------------
+  float xs[NQ];
+  const bool notpd = wave_chol_solve<NQ, true>(acc, bacc, reinterpret_cast<float*>(st), xs);
+  WAVE_STAMP(ridx, 2);
+  bool nonfinite = false;
+#pragma unroll
+  for (int A = 0; A < NQ; ++A) {
+    const int c = 16 * A + i16;
+    const float v = c < a.kreal ? xs[A] : 0.f;
+    nonfinite |= !isfinite(v);
+    if (q == 0) a.X[(int64_t)j * KP + c] = v;
   }
+  WAVE_STAMP(ridx, 3);
+  const bool bad = notpd || __any(nonfinite);  // wave-uniform
+  if (lane == 0 && bad) atomicOr(a.err, 2 | ALBEDO_EF_WAVE);
 }
 
 template <int KP>
@@ -450,16 +383,7 @@ hipError_t launch_wave_kp(const SolveArgs& a, hipStream_t s) {
   static const hipError_t attr4 = allow_lds(solve_wave_kernel<KP, false, true>, W::LDS);
   for (hipError_t e : {attr, attr2, attr3, attr4})
     if (e != hipSuccess) return e;
-  // persistent grid: the workgroups that fit at once (2 per CU at KP = 128), never more than the rows
-  static const int per_cu = [] {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, solve_wave_kernel<KP, true, true>, 64 * W::WAVES, W::LDS) !=
-            hipSuccess || n < 1)
-      n = 1;
-    return n;
-  }();
-  const int64_t want = (a.n_rows + W::WAVES - 1) / W::WAVES;
-  const int blocks = (int)std::min<int64_t>(want, (int64_t)per_cu * std::max(1, a.n_cu));
+  const int blocks = (int)((a.n_rows + W::WAVES - 1) / W::WAVES);
   if (a.Zhl) {
     if (a.implicit) solve_wave_kernel<KP, true, true><<<blocks, 64 * W::WAVES, W::LDS, s>>>(a);
     else solve_wave_kernel<KP, false, true><<<blocks, 64 * W::WAVES, W::LDS, s>>>(a);
@@ -482,21 +406,19 @@ __global__ __launch_bounds__(256, 2) void wave_partial_kernel(SolveArgs a, Split
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63, q = lane >> 4, i16 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  float* s_cs = reinterpret_cast<float*>(lds + W::WAVES * (W::LDS_WAVE + W::SCR));
+  float* s_cs = reinterpret_cast<float*>(lds + W::WAVES * W::LDS_WAVE);
   for (int e = threadIdx.x; e < 2 * KP; e += 256) s_cs[e] = a.colscale[e];
   __syncthreads();
   const int64_t slot = (int64_t)blockIdx.x * W::WAVES + wave;
   if (slot >= sp.n_chunks) return;
   char* st = lds + wave * W::LDS_WAVE;
-  float* scr = reinterpret_cast<float*>(lds + W::WAVES * W::LDS_WAVE + wave * W::SCR);
   const int j = sp.chunk_row[slot];
   const int64_t rp0 = a.ptr[j], off = (int64_t)sp.chunk_idx[slot] * sp.chunk_len;
   const int64_t rest = a.ptr[j + 1] - rp0 - off;
   const int d = (int)(rest < sp.chunk_len ? rest : sp.chunk_len);
   f32x4 acc[NT];
   float bacc[NQ];
-  WaveFeed f;  // one chunk per wave: no next row
-  const int npos = wave_build<KP, IMPLICIT, PRE>(a, rp0 + off, d, st, scr, s_cs, acc, bacc, f, lane);
+  const int npos = wave_build<KP, IMPLICIT, PRE>(a, rp0 + off, d, st, s_cs, acc, bacc);
   float* out = sp.partial + slot * R::FLOATS;
   const float* isc = s_cs + KP;
   static_for<0, NQ>([&](auto AA) {

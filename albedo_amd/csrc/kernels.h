@@ -9,6 +9,11 @@ namespace albedo {
 // Padded rank used on device: factor rows are KP floats (zero beyond `rank`).
 int padded_rank(int rank);  // 64, 128 or 256 (0 if unsupported)
 
+// *SolveArgs::err bits: 1 = a non-positive diagonal (λn + Λ), 2 = a collapsed pivot / non-finite
+// solution; with 2 the path that met it (reported in the not-positive-definite message)
+constexpr int ALBEDO_EF_LIGHT16 = 16, ALBEDO_EF_LIGHT_REG = 32, ALBEDO_EF_LIGHT_ACC = 64, ALBEDO_EF_WAVE = 128,
+              ALBEDO_EF_HEAVY = 256;
+
 struct SolveArgs {
   const float* Z;          // src factors in the eigenbasis of the src Gram, [*][KP]
   const int64_t* ptr;      // dst CSR row pointer (global dst row index)
@@ -182,6 +187,7 @@ hipError_t topk_prepare(int KP, int kreal, const float* T, int64_t n_dst, float 
                         size_t temp_bytes, uint32_t* keys, uint32_t* perm, uint32_t* nperm, double* tp, void* Th,
                         float* cfeat, float* supf, void* probe, hipStream_t s);
 hipError_t launch_topk(int KP, const TopkArgs& a, int n_cu, hipStream_t s);
+hipError_t launch_topk_select(int KP, const TopkArgs& a, hipStream_t s);  // after launch_topk (the scan)
 // starting thresholds + features + scan order of the src rows: keys / order 2·n_src uint32,
 // thr_tmp / thr_sorted n_src floats, sf_tmp / sf_sorted n_src·TOPK_SF floats
 size_t topk_order_temp_bytes(int64_t n_src);

@@ -178,7 +178,7 @@ __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB,
     const float yc = bc16<c>(y * dg);
     y = (i16 > c) ? fmaf(-kr[c], yc, y) : ((i16 == c) ? yc : y);
   });
-  if (notpd && lane == 0) atomicOr(a.err, 2);
+  if (notpd && lane == 0) atomicOr(a.err, 2 | ALBEDO_EF_LIGHT16);
   // Lᵀ v = y: lane i needs column i of L (transposed through the scratch)
   if (g == 0) {
 #pragma unroll

@@ -719,7 +719,9 @@ __global__ __launch_bounds__(256) void topk_mask_kernel(TopkArgs a, int rwg, con
 // merged at the end.  P = 1 serves the rows the MFMA pre-selection could not certify; P up to 8
 // serves k up to 512 (recommendForAll* with k > 64, no pre-selection).  The dst rows are visited in
 // the prepared chunk order and a chunk whose bound (+ F2J rounding) is below the wave's own 64·P-th
-// best is skipped: none of its rows can enter the merged top-k (<= 64·P), ties included.
+// best is skipped: none of its rows can enter the merged top-k (<= 64·P), ties included.  The bounds
+// are evaluated 64 chunks at a time (a lane per chunk), so a pruned chunk costs a fraction of one
+// feature-load latency instead of a dependent load per 64 rows.
 template <int KP, int P>
 __global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32_t* rows, int64_t row0) {
   __shared__ float msc[4][64 * P];
@@ -762,20 +764,14 @@ __global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32
     sfe[TOPK_M] = __double2float_ru(sqrt(fmax(nn - pp, 0.0) + 1e-13 * nn));
     marg = (float)(1.2e-5 * sqrt(nn) * (double)a.tmax_norm) * 1.0001f + 1e-30f;
   }
-  const int ch = topk_chunk_rows_dev<KP>();
-  for (int64_t j0 = (int64_t)wave * 64; j0 < a.n_dst; j0 += 256) {
-    if (a.cfeat && thr > -INFINITY) {
-      float b = -INFINITY;
-      for (int64_t c = j0 / ch; c <= (j0 + 63) / ch && c < a.n_chunks; ++c) b = fmaxf(b, tk_bound(sfe, a.cfeat + c * TOPK_CF));
-      if (b + marg < thr) continue;
-    }
-    const int64_t pj = j0 + lane;
-    const int64_t dj = (a.perm && pj < a.n_dst) ? (int64_t)a.perm[pj] : pj;
-    const float sc = pj < a.n_dst ? f2j_dot_v4(s, a.T + dj * KP, a.kreal) : -INFINITY;
-    if (!__any(sc >= thr)) continue;
+  // 64 dst rows (one per lane) -> F2J scores, buffered when one of them reaches the threshold
+  auto score64 = [&](int64_t pj, bool in) {
+    const int64_t dj = (a.perm && in) ? (int64_t)a.perm[pj] : pj;
+    const float sc = in ? f2j_dot_v4(s, a.T + dj * KP, a.kreal) : -INFINITY;
+    if (!__any(sc >= thr)) return;
     static_for<0, P>([&](auto hh) {
       constexpr int h = decltype(hh)::value;
-      if (nin == h) { bs[P + h] = sc; bi[P + h] = pj < a.n_dst ? (int)dj : -1; }
+      if (nin == h) { bs[P + h] = sc; bi[P + h] = in ? (int)dj : -1; }
     });
     if (++nin == P) {
       wave_bitonic<2 * P>(bs, bi);
@@ -784,6 +780,30 @@ __global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32
       nin = 0;
       thr = fmaxf(thr_init, rdlane(bs[P - 1], 63));
     }
+  };
+  if (a.cfeat) {
+    // chunk-major: each lane tests the bound of one of the wave's next 64 chunks (one feature load
+    // latency per 64 chunks, not per chunk), then the wave scores the rows of the chunks that pass,
+    // re-testing each against the threshold as it rises
+    const int ch = topk_chunk_rows_dev<KP>();
+    for (int64_t c0 = (int64_t)wave * 64; c0 < a.n_chunks; c0 += 256) {
+      const int64_t c = c0 + lane;
+      float b = INFINITY;
+      if (c < a.n_chunks) b = tk_bound(sfe, a.cfeat + c * TOPK_CF) + marg;
+      uint64_t m = __ballot(c < a.n_chunks && !(b < thr));
+      while (m) {
+        const int l = __builtin_ctzll(m);
+        m &= m - 1;
+        if (rdlane(b, l) < thr) continue;  // the threshold rose past this chunk's bound
+        const int64_t cc = c0 + l;
+        for (int r0 = 0; r0 < ch; r0 += 64) {
+          const int64_t pj = cc * ch + r0 + lane;
+          score64(pj, r0 + lane < ch && pj < a.n_dst);
+        }
+      }
+    }
+  } else {
+    for (int64_t j0 = (int64_t)wave * 64; j0 < a.n_dst; j0 += 256) score64(j0 + lane, j0 + lane < a.n_dst);
   }
   wave_bitonic<2 * P>(bs, bi);
 #pragma unroll
@@ -999,9 +1019,7 @@ hipError_t launch_topk_kp(const TopkArgs& a, int n_cu, hipStream_t s) {
   if (rows == 512) e = launch_scan<KP, (KP <= 128 ? 8 : 4)>(a, s);
   else if (rows == 256) e = launch_scan<KP, 4>(a, s);
   else e = launch_scan<KP, 2>(a, s);
-  if (e != hipSuccess) return e;
-  topk_select_kernel<KP><<<(int)((a.n_src + 3) / 4), 256, 0, s>>>(a);
-  return hipGetLastError();
+  return e;
 }
 
 hipError_t launch_topk(int KP, const TopkArgs& a, int n_cu, hipStream_t s) {
@@ -1010,6 +1028,16 @@ hipError_t launch_topk(int KP, const TopkArgs& a, int n_cu, hipStream_t s) {
   if (KP == 128) return launch_topk_kp<128>(a, n_cu, s);
   if (KP == 256) return launch_topk_kp<256>(a, n_cu, s);
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_topk_select(int KP, const TopkArgs& a, hipStream_t s) {
+  if (a.n_src <= 0) return hipSuccess;
+  const int blocks = (int)((a.n_src + 3) / 4);
+  if (KP == 64) topk_select_kernel<64><<<blocks, 256, 0, s>>>(a);
+  else if (KP == 128) topk_select_kernel<128><<<blocks, 256, 0, s>>>(a);
+  else if (KP == 256) topk_select_kernel<256><<<blocks, 256, 0, s>>>(a);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
 }
 
 // max_r ||T[r][0..kreal)||_2 (fp64), stored as the bits of a non-negative double

@@ -201,6 +201,34 @@ def read_starring(path: str, columns=STARRING_COLUMNS) -> dict:
     parts = _data_files(path) if os.path.isdir(path) else [path]
     if not parts:
         raise ValueError(f"Unable to infer schema for Parquet: {path} holds no parquet data files")
+    # Parts with one schema and no nulls (what Spark's writer and write_starring produce): row counts
+    # from the footers -> one output array per column, each part decoded by a pool thread straight
+    # into its slice (pyarrow releases the GIL; no concatenation copy).  Anything else takes the
+    # per-part read + np.concatenate (numpy's promotion of mixed types, NaN for nulls).
+    from concurrent.futures import ThreadPoolExecutor
+    files = [pq.ParquetFile(f) for f in parts]
+    schemas = [pf.schema_arrow for pf in files]
+    uniform = all(s.field(c).type == schemas[0].field(c).type for s in schemas for c in columns)
+    if uniform and len(parts) > 1:
+        counts = [pf.metadata.num_rows for pf in files]
+        offs = np.r_[0, np.cumsum(counts)].astype(np.int64)
+        out = {}
+        for c in columns:
+            dt = schemas[0].field(c).type.to_pandas_dtype()
+            out[c] = np.empty(int(offs[-1]), "datetime64[us]" if np.dtype(dt).kind == "M" else dt)
+
+        def part(i):
+            t = pq.read_table(parts[i], columns=list(columns))
+            if t.num_rows != counts[i] or any(t.column(c).null_count for c in columns):
+                return False
+            for c in columns:
+                a = t.column(c).to_numpy()
+                out[c][offs[i]:offs[i + 1]] = a.astype("datetime64[us]") if a.dtype.kind == "M" else a
+            return True
+
+        with ThreadPoolExecutor(max_workers=max(1, min(16, len(parts), os.cpu_count() or 1))) as ex:
+            if all(ex.map(part, range(len(parts)))):
+                return out
     cols = {c: [] for c in columns}
     for f in parts:
         t = pq.read_table(f, columns=list(columns))

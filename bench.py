@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 CONFIG_RANK = {"c2": 64, "c4": 128, "c1p": 50, "c5": 256}
 NONNEGATIVE = {"c5"}  # BASELINE config 5: rank 256, nonnegative=true (NNLS), extreme repo skew
 METRIC = "implicit-ALS interactions/sec per sweep at rank 128 (1/8 GPU); top-30 recs users/sec"
+MFMA_F16_TFLOPS = 2500.0  # dense fp16 MFMA peak, MI355X (MI355X_MICROARCH.md: ~2.5 PF dense)
 
 
 def parse():
@@ -200,6 +201,8 @@ def main():
                                   L.ptr(out_i, C.c_int32), L.ptr(out_s, C.c_float)))  # warm
         st0 = np.zeros(4, np.int64)
         L.check(lib.als_topk_stats(h, L.ptr(st0, C.c_int64)))
+        tm0 = np.zeros(5, np.float64)
+        L.check(lib.als_topk_timing(h, L.ptr(tm0, C.c_double)))
         barrier()
         t1 = time.perf_counter()
         # every user: recommendForAllUsers (subset = NULL); else ALSModel.recommendForUserSubset
@@ -216,9 +219,19 @@ def main():
         st1 = np.zeros(4, np.int64)
         L.check(lib.als_topk_stats(h, L.ptr(st1, C.c_int64)))
         dst = st1 - st0
+        tm1 = np.zeros(5, np.float64)
+        L.check(lib.als_topk_timing(h, L.ptr(tm1, C.c_double)))
+        tm = tm1 - tm0
+        scan_tflops = tm[4] / max(tm[1], 1e-9) / 1e9  # flops / ms -> TFLOP/s
         topk_info = {"users": int(sub.size), "all_users": bool(every), "seconds": topk_s,
                      "sweeps_before_topk": args.warmup + args.steps, "exact_rescan_rows": int(dst[1]),
                      "dst_chunks_scanned_frac": float(dst[2]) / max(1, int(dst[3])),
+                     "device_ms": {"order_mask": tm[0], "scan": tm[1], "select": tm[2], "exact": tm[3]},
+                     # the dominant kernel (the fp16 MFMA scan): scanned flops / its time vs the dense
+                     # fp16 MFMA peak (this rank's share; HIP events on the engine stream)
+                     "roofline": {"bound": "mfma", "achieved": scan_tflops, "peak": MFMA_F16_TFLOPS,
+                                  "unit": "TFLOP/s", "frac": scan_tflops / MFMA_F16_TFLOPS,
+                                  "scan_tflop": tm[4] / 1e12, "kernel": "topk_scan"},
                      "note": "wall time of als_recommend(k=30) on the user subset: dst norm sort + fp16 pack, "
                              "MFMA scan with norm-order early exit, exact F2J rescoring, D2H of the lists"}
 

@@ -179,6 +179,11 @@ int als_solver_stats(const als_ctx* ctx, int dst_side, int64_t* out4);
  * out[2] = dst rows scanned (summed over the scan waves), out[3] = the same without the norm-order
  * early exit. */
 int als_topk_stats(const als_ctx* ctx, int64_t* out4);
+/* Top-k device time since als_create, from HIP events on the context's stream (ms): out[0] = scan
+ * order + chunk masks, out[1] = the MFMA scan, out[2] = select + certification, out[3] = exact
+ * rescans; out[4] = the flops the scan's MFMAs performed (2·KP per scored src x dst pair), so
+ * out[4] / out[1] is the scan's achieved matrix rate. */
+int als_topk_timing(const als_ctx* ctx, double* out5);
 /* The src ids whose candidate set failed certification in the last als_recommend call (k <= 64) and
  * were re-scored by the exact scan, in output order; *n_out = their count, ids filled when
  * n_out <= cap.  Parity tests check exactly these rows against the oracle. */

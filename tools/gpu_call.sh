@@ -35,7 +35,12 @@ for s in "$@"; do
     c1p) timeout -k 10 900 python -u tools/c1p_job.py --out gpurun_out/c1p_job.json > gpurun_out/c1p_job.log 2>&1 ;;
     tests_eig) timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "device_eigensolver or half_sweep_ranks" > gpurun_out/tests_eig.log 2>&1 ;;
     bench_c4q) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 > gpurun_out/bench_c4q.json 2> gpurun_out/bench_c4q.err ;;
-    factortime) (cd tools/probe && timeout -k 5 120 ./factortime 1000000) > gpurun_out/factortime.txt 2>&1 ;;
+    bench_c4q_l*) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 --light ${s#bench_c4q_l} > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
+    ab_*) # A/B: the quick c4 bench on tools/ab/<name>.so in place of the built library, then restored
+      n=${s#ab_}; cp albedo_amd/libalbedo_als.so /tmp/albedo_main.so && cp tools/ab/$n.so albedo_amd/libalbedo_als.so && \
+      { timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err; r=$?; cp /tmp/albedo_main.so albedo_amd/libalbedo_als.so; [ $r -eq 0 ]; } ;;
+    debug_c1) timeout -k 10 300 python -u tools/debug_c1.py > gpurun_out/debug_c1.log 2>&1 ;;
+    factortime)(cd tools/probe && timeout -k 5 120 ./factortime 1000000) > gpurun_out/factortime.txt 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

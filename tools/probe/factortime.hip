@@ -4,6 +4,7 @@
 //   ./factortime NROWS
 #define WAVE_PROBE_STAMPS
 #define WAVE_PROBE_FACTOR_ONLY
+#define WAVE_PROBE_CHOL_PHASES
 #include "../../albedo_amd/csrc/heavy_wave.hip"
 #include <cstdio>
 #include <cstdlib>
@@ -19,6 +20,9 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&lam, KP * 4)); CK(hipMalloc(&cs, 2 * KP * 4)); CK(hipMalloc(&err, 4));
   CK(hipMalloc(&stamps, nrows * 4 * 8));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(g_wave_stamps), &stamps, sizeof(stamps)));
+  unsigned long long* ph;
+  CK(hipMalloc(&ph, nrows * 8 * 8));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(g_chol_ph), &ph, sizeof(ph)));
   std::vector<int64_t> hp(nrows + 1); std::vector<int32_t> hr(nrows);
   for (int64_t i = 0; i <= nrows; ++i) hp[i] = i * 80;
   for (int64_t i = 0; i < nrows; ++i) hr[i] = (int32_t)i;
@@ -53,6 +57,13 @@ int main(int argc, char** argv) {
       sf += (double)(t[2] - t[1]);
       ++n;
     }
+    std::vector<unsigned long long> hph(nrows * 8);
+    CK(hipMemcpy(hph.data(), ph, hph.size() * 8, hipMemcpyDeviceToHost));
+    double pa[8] = {0}; int64_t pn = 0;
+    for (int64_t i = 0; i < nrows; i += 7, ++pn)
+      for (int q = 0; q < 8; ++q) pa[q] += (double)hph[i * 8 + q];
+    printf("  phases (cycles/row): diag-to-rows %.0f  diag_block %.0f  linv-image %.0f  panel-U %.0f  rhs %.0f  trailing %.0f  back-sub %.0f\n",
+           pa[0] / pn, pa[1] / pn, pa[2] / pn, pa[3] / pn, pa[4] / pn, pa[5] / pn, pa[6] / pn);
     int herr = 0; CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
     printf("waves/SIMD %d: %8.3f ms for %lld rows (%.1f ns/row), factor cycles/row %.0f, err %d\n", occ, ms,
            (long long)nrows, ms * 1e6 / nrows, n ? sf / n : 0.0, herr);
