@@ -106,6 +106,7 @@ SIGNATURES = [
     ("als_solver_stats", C.c_int, [P, C.c_int, I64P]),
     ("als_topk_stats", C.c_int, [P, I64P]),
     ("als_topk_timing", C.c_int, [P, F64P]),
+    ("als_get_basis", C.c_int, [P, C.c_int, F64P]),
     ("als_topk_last_rescan", C.c_int, [P, I32P, C.c_int64, I64P]),
     ("als_synchronize", C.c_int, [P]),
     ("als_synth_generate", C.c_int, [C.c_int32, C.c_uint64, C.c_int32, C.c_int64, C.c_int64, I64P, F64P, I32P,

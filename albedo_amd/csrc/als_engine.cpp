@@ -1384,6 +1384,20 @@ int als_fit(als_ctx* c) {
   return als_run_sweeps(c, c->p.max_iter);
 }
 
+int als_get_basis(als_ctx* c, int side, double* out) {
+  if (!c || (side != 0 && side != 1) || !out) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  const Side& S = c->s[side];
+  if (!S.d_B.p) return fail(ALS_E_STATE, "no factors yet");
+  TRYC(set_device(c));
+  const int k = c->p.rank, KP = c->KP;
+  std::vector<double> B((size_t)KP * KP);
+  HIPCHK(hipMemcpyAsync(B.data(), S.d_B.p, B.size() * 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  for (int i = 0; i < k; ++i)
+    for (int j = 0; j < k; ++j) out[(size_t)i * k + j] = B[(size_t)i * KP + j];
+  return ALS_OK;
+}
+
 int als_get_gram(als_ctx* c, int src_side, double* out) {
   if (!c || (src_side != 0 && src_side != 1) || !out) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
   const Side& S = c->s[src_side];

@@ -308,6 +308,11 @@ __global__ __launch_bounds__(256) void eig_finish_kernel(const double* __restric
     }
 }
 
+__global__ void ns_combine_kernel(double* __restrict__ WT, const double* __restrict__ M, int n) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) WT[e] = 1.5 * WT[e] - 0.5 * M[e];
+}
+
 __global__ void identity_kernel(double* __restrict__ B, int KP) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e < KP * KP) B[e] = (e / KP == e % KP) ? 1.0 : 0.0;
@@ -334,6 +339,14 @@ hipError_t launch_device_eig(int KP, int k, const double* G, const double* Bs, c
   int* sweeps = reinterpret_cast<int*>(wmm + 2);
   const int g = (KP * KP + 255) / 256;
   dgemm_kp_kernel<true, false><<<g, 256, 0, s>>>(Bt_in, Bs, WT, KP);  // Wᵀ = B_tᵀ B_s
+  // One Newton-Schulz step towards the orthogonal polar factor: Wᵀ <- (3 Wᵀ - Wᵀ W Wᵀ) / 2.  Without it
+  // the warm start couples the two bases' orthogonality errors (P = W·J inherits both, B_t = B_s·P
+  // adds them again): they grow ~2.5x per half-sweep, and after ~40 halves the rotated Gram is no
+  // longer the Gram of the original factors (measured: tools/debug_c1.py).  One step squares the
+  // error (W is orthogonal to rounding plus the previous half's drift).
+  dgemm_kp_kernel<false, true><<<g, 256, 0, s>>>(WT, WT, T, KP);     // Wᵀ W
+  dgemm_kp_kernel<false, false><<<g, 256, 0, s>>>(T, WT, M, KP);     // Wᵀ W Wᵀ
+  ns_combine_kernel<<<g, 256, 0, s>>>(WT, M, KP * KP);
   dgemm_kp_kernel<false, true><<<g, 256, 0, s>>>(G, WT, T, KP);      // G W
   dgemm_kp_kernel<false, false><<<g, 256, 0, s>>>(WT, T, M, KP);     // Wᵀ G W
   if (k <= 128) {
@@ -346,6 +359,13 @@ hipError_t launch_device_eig(int KP, int k, const double* G, const double* Bs, c
   }
   eig_finish_kernel<<<std::max(1, std::min(64, g)), 256, 0, s>>>(w, WT, k, KP, P32, lam32, ub, wmm);
   dgemm_kp_kernel<false, true><<<g, 256, 0, s>>>(Bs, WT, Bt_out, KP);  // B_t = B_s P = B_s (Vᵀ)ᵀ
+  // and one Newton-Schulz step on B_t itself: the rotations' roundings (c² + s² = 1 + O(u), a few
+  // hundred per row and half-sweep) would otherwise grow the columns' norms linearly over a fit
+  // (1e-12 after 60 halves, measured); B_t <- B_t (3I - B_tᵀ B_t) / 2 keeps both bases orthogonal to
+  // rounding for any fit length
+  dgemm_kp_kernel<true, false><<<g, 256, 0, s>>>(Bt_out, Bt_out, T, KP);  // B_tᵀ B_t
+  dgemm_kp_kernel<false, false><<<g, 256, 0, s>>>(Bt_out, T, M, KP);     // B_t B_tᵀ B_t
+  ns_combine_kernel<<<g, 256, 0, s>>>(Bt_out, M, KP * KP);
   return hipGetLastError();
 }
 

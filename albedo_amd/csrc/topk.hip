@@ -357,7 +357,8 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       const float tkt = rdlane(s2[0], a.kt - 1);  // the running kt-th best becomes the threshold
       if (lane == 0) s_thr[wr0 + wl] = tkt;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (the compacted lists' stores need no wait here: later appends go to other slots, and the next
+    // compaction waits for every store of this wave before it reads a list back)
     WAVE_LDS_SYNC();
 #pragma unroll
     for (int gi = 0; gi < G; ++gi)
@@ -372,22 +373,9 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       }
   };
 
-  int64_t it = 0;
-  for (int64_t c = next_chunk(-1); c < nch; c = next_chunk(c), ++it) {
-    // this wave's DMAs of chunk c have landed (in-order VM counter; later list stores only make the
-    // wait stricter), then one barrier publishes every wave's part and retires the previous slot
-    if (n_iss - it - 1 >= C::NSTG - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NVM * (C::NSTG - 2)) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (c_iss < nch) {
-      c_iss = next_chunk(c_iss);
-      if (c_iss < nch) {
-        dma(c_iss, (int)((it + C::NSTG - 1) % C::NSTG));
-        ++n_iss;
-      }
-    }
-    // can any row of this wave still take a dst row of chunk c (bound + margin >= its threshold)?
+  // one chunk: can any row of this wave still take a dst row of chunk c (bound + margin >= its
+  // threshold)?  then the MFMA scores of the wave's rows against the chunk's rows, tile by tile
+  auto scan_chunk = [&](int64_t c, int64_t it) __attribute__((always_inline)) {
     const char* base = ring + (int)(it % C::NSTG) * C::SLOT;
     bool need = !a.cfeat;
     if (a.cfeat) {
@@ -408,7 +396,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
         }
       }
     }
-    if (!__any(need)) continue;
+    if (!__any(need)) return;
     const int64_t j0 = c * C::CH;
     f16x8 df[2][NQ];
     auto rd = [&](int J, f16x8 (&d)[NQ]) __attribute__((always_inline)) {
@@ -431,6 +419,28 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       if constexpr (J > 0) check_tile(acc[(J - 1) & 1], j0 + 16 * (J - 1));
     });
     check_tile(acc[(NJ - 1) & 1], j0 + 16 * (NJ - 1));
+  };
+
+  int64_t it = 0;
+  for (int64_t c = next_chunk(-1); c < nch; c = next_chunk(c), ++it) {
+    // this wave's DMAs of chunk c have landed (in-order VM counter; later list stores only make the
+    // wait stricter), then one barrier publishes every wave's part and retires the previous slot
+    if (n_iss - it - 1 >= C::NSTG - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NVM * (C::NSTG - 2)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    scan_chunk(c, it);
+    // the next DMA goes out after this chunk's list stores and compactions: a compaction waits for
+    // this wave's stores (vmcnt(0), in-order counter), and a DMA issued before them would have to
+    // land first -- a full HBM latency per compaction.  Its slot held chunk it - 1, free since the
+    // barrier above.
+    if (c_iss < nch) {
+      c_iss = next_chunk(c_iss);
+      if (c_iss < nch) {
+        dma(c_iss, (int)((it + C::NSTG - 1) % C::NSTG));
+        ++n_iss;
+      }
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup ends
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

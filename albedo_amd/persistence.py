@@ -154,8 +154,9 @@ def load_als_model(path: str):
 STARRING_COLUMNS = ("user_id", "repo_id", "starred_at", "starring")
 
 
-def write_starring(path: str, stars: dict, rows_per_part: int = 1 << 24) -> None:
-    """`df.write.mode("overwrite").parquet(path)` of a Starring dataset (INT96 timestamps)."""
+def write_starring(path: str, stars: dict, rows_per_part: int = 1 << 24, workers: int = 1, progress=None) -> None:
+    """`df.write.mode("overwrite").parquet(path)` of a Starring dataset (INT96 timestamps).  `workers`
+    parts are encoded at once (pyarrow releases the GIL); `progress(done, total)` after each part."""
     import pyarrow as pa
     import pyarrow.parquet as pq
     if os.path.exists(path):
@@ -168,7 +169,9 @@ def write_starring(path: str, stars: dict, rows_per_part: int = 1 << 24) -> None
                         pa.field("starred_at", pa.timestamp("us")), pa.field("starring", pa.float64(), nullable=False)])
     n = len(stars["user_id"])
     job = uuid.uuid4()
-    for p in range(max(1, -(-n // rows_per_part))):
+    nparts = max(1, -(-n // rows_per_part))
+
+    def part(p):
         lo, hi = p * rows_per_part, min(n, (p + 1) * rows_per_part)
         t = pa.Table.from_arrays([pa.array(np.asarray(stars["user_id"][lo:hi], np.int32)),
                                   pa.array(np.asarray(stars["repo_id"][lo:hi], np.int32)),
@@ -176,6 +179,18 @@ def write_starring(path: str, stars: dict, rows_per_part: int = 1 << 24) -> None
                                   pa.array(np.asarray(stars["starring"][lo:hi], np.float64))], schema=schema)
         pq.write_table(t, os.path.join(path, f"part-{p:05d}-{job}-c000.snappy.parquet"), compression="snappy",
                        use_deprecated_int96_timestamps=True)
+
+    if workers <= 1:
+        for p in range(nparts):
+            part(p)
+            if progress:
+                progress(p + 1, nparts)
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=workers) as ex:
+            for i, _ in enumerate(ex.map(part, range(nparts))):
+                if progress:
+                    progress(i + 1, nparts)
     _finish(path)
 
 

@@ -128,6 +128,10 @@ int als_get_row_ratings(als_ctx* ctx, int side, int32_t id, int64_t cap, int32_t
 /* Ratings per row of `side` in ascending id order (this rank's rows; -1 for rows other ranks own).
  * Observability for the power-law skew (the per-row work of Spark's computeFactors). */
 int als_get_degrees(const als_ctx* ctx, int side, int64_t* out);
+/* The orthogonal basis B of side's factors (rank x rank, row-major): original factors = X·Bᵀ, X the
+ * factors as the engine holds them (als_get_factors returns the original ones).  Implicit fits
+ * rotate every half-sweep's solution into the eigenbasis of the src Gram (B_t = B_s·P). */
+int als_get_basis(als_ctx* ctx, int side, double* out);
 /* Debug/parity: the last Gram matrix YᵀY of `src_side` in the original basis (fp64, [rank][rank];
  * Spark computeYtY of the src factors the last half-sweep solved from). */
 int als_get_gram(als_ctx* ctx, int src_side, double* out);

@@ -782,6 +782,32 @@ def test_nnls_lockstep_light_rows(gpu_lib, monkeypatch, k, wgs):
     assert np.mean((U == 0) == (U_ref == 0)) > 0.995
 
 
+@pytest.mark.parametrize("k", [50, 128])
+def test_bases_stay_orthogonal_over_many_sweeps(gpu_lib, k):
+    """The warm-started device eigensolver chains the bases (W = B_sᵀB_t, B_t <- B_s·W·J): both must
+    stay orthogonal to rounding over a long fit (their errors were once coupled and grew ~2.5x per
+    half-sweep), and the last half must still match the fp64 solve from the device's own factors."""
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(3000, 800, 40000, seed=90 + k))
+    B = O.make_blocks(d["user"], d["item"], d["rating"])
+    c = Ctx(gpu_lib, k)
+    c.ratings(d["user"], d["item"], d["rating"])
+    rng = np.random.default_rng(k)
+    c.inject(0, B.user_ids, (rng.standard_normal((len(B.user_ids), k)) * 0.1).astype(np.float32))
+    c.inject(1, B.item_ids, np.zeros((len(B.item_ids), k), np.float32))
+    for h in range(60):
+        c.half(1 - (h % 2))
+    for side in (0, 1):
+        b = np.zeros((k, k))
+        c.L.check(gpu_lib.als_get_basis(c.h, side, c.L.ptr(b, C.c_double)))
+        assert np.abs(b.T @ b - np.eye(k)).max() < 1e-13, side
+    _, V = c.factors(1)
+    c.half(0)
+    U_ref = O.half_sweep(V, B.u_ptr, B.u_col, B.u_val, reg=0.5, alpha=40.0)
+    _, U = c.factors(0)
+    assert _row_rel(U, U_ref) < 1e-4
+
+
 @pytest.mark.parametrize("k", [50, 128, 200])
 def test_device_eigensolver(gpu_lib, k):
     """The half-sweep's device eigensolver (eig.hip, warm-started cyclic Jacobi in fp64) on Grams of

@@ -146,3 +146,37 @@ def test_rotate_isa_check_on_built_object():
     last = max(n for n, i in enumerate(ins) if i.startswith("global_load_dwordx4"))
     reg = ins[last].split()[1].rstrip(",")
     assert "read before" in cri.check(ins[:last + 1] + [f"v_mov_b32 v200, {reg.replace('[', '').split(':')[0]}"] + ins[last + 1:])
+
+
+def test_warm_started_jacobi_chain_keeps_bases_orthogonal():
+    """eig.hip's basis chain in numpy (tools/jacobi_ref.py): W = B_sᵀB_t, one Newton-Schulz step,
+    Jacobi of WᵀGW from Wᵀ, B_t <- B_s·P and a Newton-Schulz step on B_t.  Over 40 halves of
+    slowly drifting Grams the bases stay orthogonal to rounding and every P diagonalises its Gram;
+    the warm start needs fewer sweeps than a cold one."""
+    from tools.jacobi_ref import jacobi
+    rng = np.random.default_rng(3)
+    k = 24
+    Q, _ = np.linalg.qr(rng.standard_normal((k, k)))
+    w = np.logspace(-1, 3, k)
+    bases = [np.eye(k), np.eye(k)]  # user, item
+
+    def ns(A):
+        return 1.5 * A - 0.5 * A @ (A.T @ A)
+
+    sweeps = []
+    for h in range(40):
+        t, s = 1 - (h % 2), h % 2
+        Q = Q @ np.linalg.qr(np.eye(k) + 1e-3 * rng.standard_normal((k, k)))[0]  # the Gram drifts
+        G_orig = (Q * w) @ Q.T
+        Bs, Bt = bases[s], bases[t]
+        Gb = Bs.T @ G_orig @ Bs  # the Gram as the engine forms it (factors in basis B_s)
+        WT = ns(Bt.T @ Bs)  # Wᵀ = B_tᵀ B_s, orthogonalised
+        M = WT @ Gb @ WT.T
+        lam, VT, sw = jacobi(M, VT=WT)
+        sweeps.append(sw)
+        P = VT.T
+        R = P.T @ Gb @ P
+        assert np.linalg.norm(R - np.diag(np.diag(R))) < 1e-12 * np.linalg.norm(Gb)
+        bases[t] = ns(Bs @ P)
+        assert np.abs(bases[t].T @ bases[t] - np.eye(k)).max() < 1e-13
+    assert max(sweeps[4:]) < sweeps[0]

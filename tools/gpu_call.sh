@@ -32,14 +32,17 @@ for s in "$@"; do
     tests_mr) timeout -k 10 900 $PYT tests/test_multi_rank.py > gpurun_out/tests_mr.log 2>&1 ;;
     wavetime) (cd tools/probe && timeout -k 5 120 ./wavetime 20000000 80,160,320,640,1280,4096 200000000 && timeout -k 5 120 ./wavetime_bo 20000000 80,160,320,640,1280,4096 200000000) > gpurun_out/wavetime.txt 2>&1 ;;
     wavetime1) (cd tools/probe && timeout -k 5 120 ./wavetime 20000000 80,160,320,640,1280,4096 200000000) > gpurun_out/wavetime1.txt 2>&1 ;;
+    c4ingest) timeout -k 10 900 python -u tools/c1p_job.py --config c4 --rank 128 --ingest-only --out gpurun_out/c4_ingest.json > gpurun_out/c4_ingest.log 2>&1 ;;
     c1p) timeout -k 10 900 python -u tools/c1p_job.py --out gpurun_out/c1p_job.json > gpurun_out/c1p_job.log 2>&1 ;;
-    tests_eig) timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "device_eigensolver or half_sweep_ranks" > gpurun_out/tests_eig.log 2>&1 ;;
+    tests_eig) timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "device_eigensolver or half_sweep_ranks or orthogonal" > gpurun_out/tests_eig.log 2>&1 ;;
+    bench_topk) timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk.json 2> gpurun_out/bench_topk.err ;;
     bench_c4q) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 > gpurun_out/bench_c4q.json 2> gpurun_out/bench_c4q.err ;;
     bench_c4q_l*) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 --light ${s#bench_c4q_l} > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
     ab_*) # A/B: the quick c4 bench on tools/ab/<name>.so in place of the built library, then restored
       n=${s#ab_}; cp albedo_amd/libalbedo_als.so /tmp/albedo_main.so && cp tools/ab/$n.so albedo_amd/libalbedo_als.so && \
       { timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err; r=$?; cp /tmp/albedo_main.so albedo_amd/libalbedo_als.so; [ $r -eq 0 ]; } ;;
-    debug_c1) timeout -k 10 300 python -u tools/debug_c1.py > gpurun_out/debug_c1.log 2>&1 ;;
+    debug_eig) timeout -k 10 600 python -u tools/debug_eig.py > gpurun_out/debug_eig.log 2>&1; r=$?; echo "debug_eig rc $r"; [ $r -le 1 ] ;;
+    debug_c1) timeout -k 10 300 python -u tools/debug_c1.py > gpurun_out/debug_c1.log 2>&1; r=$?; echo "debug_c1 rc $r"; [ $r -le 1 ] ;;
     factortime)(cd tools/probe && timeout -k 5 120 ./factortime 1000000) > gpurun_out/factortime.txt 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
