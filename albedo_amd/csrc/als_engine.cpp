@@ -1761,7 +1761,8 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   if (known.empty() || T.n == 0) return ALS_OK;
   TopkPlan P;
   TRYC(topk_plan(c, src, k, P));
-  const int64_t chunk = 1 << 20;
+  // 4M src rows per pass (candidate lists 4 GB): fewer launch tails than 1M-row passes
+  const int64_t chunk = 1 << 22;
   // world > 1 (SURVEY §8(e) "Top-k: shard users"): rank r scores the r-th contiguous slice of the
   // known src rows against the replicated dst factors; the lists are all-gathered afterwards
   const int64_t n_known = (int64_t)known.size();

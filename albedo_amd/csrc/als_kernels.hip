@@ -637,8 +637,10 @@ hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64
 // in the MFMA accumulators (wave_chol.h) and need its scratch (WCHOL_SCR floats + NB L⁻¹ tiles)
 __host__ __device__ constexpr int light_wave_lds(int D) { return D == 16 ? D * (D + 1) / 2 + 64 : WCHOL_SCR + (D / 16) * 256; }
 
+// workgroups per CU: D = 32 at KP = 128 keeps its gathered rows in registers (KEEPZ) and spilled 16
+// VGPRs at 4 (128 VGPRs); at 3 (168) it does not, and the user light half is 1.9 ms faster (r04 A/B)
 template <int KP, int D>
-constexpr int light_occupancy() { return (D == 16 && KP <= 128) ? 6 : (KP <= 128) ? 4 : 2; }
+constexpr int light_occupancy() { return (D == 16 && KP <= 128) ? 6 : (KP == 128 && D == 32) ? 3 : (KP <= 128) ? 4 : 2; }
 
 // One light row: j, degree d (wave-uniform), lane e < d holds rating r and src row colE of entry e.
 template <int KP, int D>

@@ -357,8 +357,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       const float tkt = rdlane(s2[0], a.kt - 1);  // the running kt-th best becomes the threshold
       if (lane == 0) s_thr[wr0 + wl] = tkt;
     }
-    // (the compacted lists' stores need no wait here: later appends go to other slots, and the next
-    // compaction waits for every store of this wave before it reads a list back)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     WAVE_LDS_SYNC();
 #pragma unroll
     for (int gi = 0; gi < G; ++gi)
@@ -373,9 +372,22 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       }
   };
 
-  // one chunk: can any row of this wave still take a dst row of chunk c (bound + margin >= its
-  // threshold)?  then the MFMA scores of the wave's rows against the chunk's rows, tile by tile
-  auto scan_chunk = [&](int64_t c, int64_t it) __attribute__((always_inline)) {
+  int64_t it = 0, n_scored = 0;  // chunk iterations; chunks this wave scored (its `need` held)
+  for (int64_t c = next_chunk(-1); c < nch; c = next_chunk(c), ++it) {
+    // this wave's DMAs of chunk c have landed (in-order VM counter; later list stores only make the
+    // wait stricter), then one barrier publishes every wave's part and retires the previous slot
+    if (n_iss - it - 1 >= C::NSTG - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NVM * (C::NSTG - 2)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (c_iss < nch) {
+      c_iss = next_chunk(c_iss);
+      if (c_iss < nch) {
+        dma(c_iss, (int)((it + C::NSTG - 1) % C::NSTG));
+        ++n_iss;
+      }
+    }
+    // can any row of this wave still take a dst row of chunk c (bound + margin >= its threshold)?
     const char* base = ring + (int)(it % C::NSTG) * C::SLOT;
     bool need = !a.cfeat;
     if (a.cfeat) {
@@ -396,7 +408,8 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
         }
       }
     }
-    if (!__any(need)) return;
+    if (!__any(need)) continue;
+    ++n_scored;
     const int64_t j0 = c * C::CH;
     f16x8 df[2][NQ];
     auto rd = [&](int J, f16x8 (&d)[NQ]) __attribute__((always_inline)) {
@@ -419,28 +432,6 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       if constexpr (J > 0) check_tile(acc[(J - 1) & 1], j0 + 16 * (J - 1));
     });
     check_tile(acc[(NJ - 1) & 1], j0 + 16 * (NJ - 1));
-  };
-
-  int64_t it = 0;
-  for (int64_t c = next_chunk(-1); c < nch; c = next_chunk(c), ++it) {
-    // this wave's DMAs of chunk c have landed (in-order VM counter; later list stores only make the
-    // wait stricter), then one barrier publishes every wave's part and retires the previous slot
-    if (n_iss - it - 1 >= C::NSTG - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NVM * (C::NSTG - 2)) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    scan_chunk(c, it);
-    // the next DMA goes out after this chunk's list stores and compactions: a compaction waits for
-    // this wave's stores (vmcnt(0), in-order counter), and a DMA issued before them would have to
-    // land first -- a full HBM latency per compaction.  Its slot held chunk it - 1, free since the
-    // barrier above.
-    if (c_iss < nch) {
-      c_iss = next_chunk(c_iss);
-      if (c_iss < nch) {
-        dma(c_iss, (int)((it + C::NSTG - 1) % C::NSTG));
-        ++n_iss;
-      }
-    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup ends
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -453,8 +444,8 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
         if (si < a.n_src) a.lcnt[si] = (int)((cntp[gi] >> (8 * r)) & 0xffu);
       }
   }
-  // dst rows streamed by the workgroup (chunks x rows x 4 waves, the full-scan unit of topk_stats)
-  if (a.scanned && tid == 0) atomicAdd(a.scanned, (unsigned long long)(it * C::CH * 4));
+  // dst rows this wave scored against its rows (topk_stats[2]: the MFMA work is 16·G src rows x these)
+  if (a.scanned && lane == 0) atomicAdd(a.scanned, (unsigned long long)(n_scored * C::CH));
 }
 
 // One wave per src row: best 64 of the list, exact F2J rescoring, sort, certify, write top-k.
@@ -651,7 +642,10 @@ hipError_t topk_order(int KP, const TopkArgs& a, void* temp, size_t temp_bytes, 
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   size_t tb = temp_bytes;
-  e = rocprim::radix_sort_pairs_desc(temp, tb, k0, k1, v0, order, (size_t)n, 0, 32, s);
+  // ascending thr0 / ‖s‖: rows with the lowest relative thresholds (the most chunks to scan, the most
+  // candidates) fill the first workgroups, which the dispatcher starts first; the light ones then fill
+  // in behind them instead of the heavy ones forming the launch's tail
+  e = rocprim::radix_sort_pairs(temp, tb, k0, k1, v0, order, (size_t)n, 0, 32, s);
   if (e != hipSuccess) return e;
   topk_gather_rows_kernel<<<tk_grid(n, 256), 256, 0, s>>>(a.src_rows, thr_tmp, sf_tmp, order, n, src_sorted,
                                                           thr_sorted, sf_sorted);
@@ -687,6 +681,31 @@ __global__ __launch_bounds__(256) void topk_mask_kernel(TopkArgs a, int rwg, con
   }
   nrow = (int)std::min<int64_t>(rwg, a.n_src - p0);
   __syncthreads();
+  // envelope of each group of MG rows: per direction the min / max of s_d, the max ‖s_⊥‖ and the
+  // smallest threshold.  tk_bound is convex in each s_d (max(s_d·lo_d, s_d·hi_d)), so its maximum
+  // over the group is at an end of [min s_d, max s_d]; fp32 rounding is monotonic, so evaluated in
+  // tk_bound's order the envelope is >= every row's bound: a group whose envelope is below its
+  // smallest threshold has no row that needs the chunk, and a chunk most groups reject costs
+  // rwg / MG envelope tests instead of rwg row tests
+  constexpr int MG = 32;
+  __shared__ float genv[512 / MG][2 * TOPK_M + 2];  // smin[M], smax[M], max ‖s_⊥‖, min threshold
+  const int ngrp = (nrow + MG - 1) / MG;
+  if (tid < ngrp) {
+    float mn[TOPK_M], mx[TOPK_M], sp = 0.f, th = INFINITY;
+#pragma unroll
+    for (int d = 0; d < TOPK_M; ++d) { mn[d] = INFINITY; mx[d] = -INFINITY; }
+    for (int i = tid * MG; i < min(nrow, tid * MG + MG); ++i) {
+#pragma unroll
+      for (int d = 0; d < TOPK_M; ++d) { mn[d] = fminf(mn[d], rf[8 * i + d]); mx[d] = fmaxf(mx[d], rf[8 * i + d]); }
+      sp = fmaxf(sp, rf[8 * i + TOPK_M]);
+      th = fminf(th, rf[8 * i + TOPK_M + 1]);
+    }
+#pragma unroll
+    for (int d = 0; d < TOPK_M; ++d) { genv[tid][d] = mn[d]; genv[tid][TOPK_M + d] = mx[d]; }
+    genv[tid][2 * TOPK_M] = sp;
+    genv[tid][2 * TOPK_M + 1] = th;
+  }
+  __syncthreads();
   auto needed = [&](const float* cf) {
     float c[TOPK_CF];
 #pragma unroll
@@ -695,8 +714,16 @@ __global__ __launch_bounds__(256) void topk_mask_kernel(TopkArgs a, int rwg, con
 #pragma unroll
       for (int e = 0; e < 4; ++e) c[f + e] = v[e];
     }
-    for (int i = 0; i < nrow; ++i)
-      if (tk_bound(rf + 8 * i, c) >= rf[8 * i + TOPK_M + 1]) return true;
+    for (int gq = 0; gq < ngrp; ++gq) {
+      const float* e = genv[gq];
+      float b = e[2 * TOPK_M] * c[2 * TOPK_M];  // tk_bound's order
+#pragma unroll
+      for (int d = 0; d < TOPK_M; ++d)
+        b += fmaxf(fmaxf(e[d] * c[d], e[d] * c[TOPK_M + d]), fmaxf(e[TOPK_M + d] * c[d], e[TOPK_M + d] * c[TOPK_M + d]));
+      if (!(b >= e[2 * TOPK_M + 1])) continue;
+      for (int i = gq * MG; i < min(nrow, gq * MG + MG); ++i)
+        if (tk_bound(rf + 8 * i, c) >= rf[8 * i + TOPK_M + 1]) return true;
+    }
     return false;
   };
   uint32_t* mrow = mask + (int64_t)blockIdx.x * a.mask_words;
@@ -963,10 +990,12 @@ int topk_chunk_rows(int KP) {
 }
 
 size_t topk_sort_temp_bytes(int64_t n) {
-  size_t tb = 0;
+  size_t tb = 0, ta = 0;
   (void)rocprim::radix_sort_pairs_desc(nullptr, tb, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                        (uint32_t*)nullptr, (size_t)n, 0, 32, (hipStream_t)0);
-  return tb;
+  (void)rocprim::radix_sort_pairs(nullptr, ta, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                  (uint32_t*)nullptr, (size_t)n, 0, 32, (hipStream_t)0);
+  return std::max(tb, ta);
 }
 
 hipError_t topk_prepare(int KP, int kreal, const float* T, int64_t n, float tsc, const double* VP, void* temp,

@@ -180,7 +180,7 @@ int als_path_stats(const als_ctx* ctx, int dst_side, int64_t* out4);
 int als_solver_stats(const als_ctx* ctx, int dst_side, int64_t* out4);
 /* Top-k counters since als_create (als_recommend with k <= 64): out[0] = src rows through the MFMA
  * scan, out[1] = rows whose candidate set failed certification and were re-scored by the exact scan,
- * out[2] = dst rows scanned (summed over the scan waves), out[3] = the same without the norm-order
+ * out[2] = dst rows the scan waves scored (a wave skips a chunk none of its rows can use), out[3] = the same without the chunk
  * early exit. */
 int als_topk_stats(const als_ctx* ctx, int64_t* out4);
 /* Top-k device time since als_create, from HIP events on the context's stream (ms): out[0] = scan

@@ -35,9 +35,13 @@ for s in "$@"; do
     c4ingest) timeout -k 10 900 python -u tools/c1p_job.py --config c4 --rank 128 --ingest-only --out gpurun_out/c4_ingest.json > gpurun_out/c4_ingest.log 2>&1 ;;
     c1p) timeout -k 10 900 python -u tools/c1p_job.py --out gpurun_out/c1p_job.json > gpurun_out/c1p_job.log 2>&1 ;;
     tests_eig) timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "device_eigensolver or half_sweep_ranks or orthogonal" > gpurun_out/tests_eig.log 2>&1 ;;
+    pmc_topk4) timeout -k 10 600 tools/pmc_topk4.sh r04 > gpurun_out/pmc_topk4.log 2>&1 ;;
     bench_topk) timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk.json 2> gpurun_out/bench_topk.err ;;
     bench_c4q) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 > gpurun_out/bench_c4q.json 2> gpurun_out/bench_c4q.err ;;
     bench_c4q_l*) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 --light ${s#bench_c4q_l} > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
+    abtk_*) # A/B of top-k: the 25-sweep + all-users top-30 bench on tools/ab/<name>.so, then restored
+      n=${s#abtk_}; cp albedo_amd/libalbedo_als.so /tmp/albedo_main.so && cp tools/ab/$n.so albedo_amd/libalbedo_als.so && \
+      { timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/abtk_$n.json 2> gpurun_out/abtk_$n.err; r=$?; cp /tmp/albedo_main.so albedo_amd/libalbedo_als.so; [ $r -eq 0 ]; } ;;
     ab_*) # A/B: the quick c4 bench on tools/ab/<name>.so in place of the built library, then restored
       n=${s#ab_}; cp albedo_amd/libalbedo_als.so /tmp/albedo_main.so && cp tools/ab/$n.so albedo_amd/libalbedo_als.so && \
       { timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err; r=$?; cp /tmp/albedo_main.so albedo_amd/libalbedo_als.so; [ $r -eq 0 ]; } ;;
