@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "host_math.h"
@@ -313,9 +314,11 @@ void spark_initialize(const int32_t* ids_sorted, int64_t n, int rank, int64_t si
     int b = (int)(((int64_t)ids_sorted[i] % num_blocks + num_blocks) % num_blocks);
     rows[b].push_back(i);
   }
-  std::vector<float> v(rank);
-  for (int b = 0; b < num_blocks; ++b) {
-    if (rows[b].empty()) continue;
+  // one generator per block, as Spark's per-block XORShiftRandom: each block's stream is sequential
+  // (the Gaussian draws are rejection-sampled), the blocks are independent -> one thread per block
+  auto block = [&](int b) {
+#pragma clang fp contract(off)
+    std::vector<float> v(rank);
     XorShift rnd((int64_t)byteswap64((uint64_t)side_seed ^ (uint64_t)b));
     for (int64_t r : rows[b]) {
       for (int c = 0; c < rank; ++c) v[c] = (float)rnd.next_gaussian();
@@ -323,7 +326,14 @@ void spark_initialize(const int32_t* ids_sorted, int64_t n, int rank, int64_t si
       const float inv = 1.0f / nrm;
       for (int c = 0; c < rank; ++c) out[r * ld + c] = v[c] * inv;
     }
-  }
+  };
+  std::vector<std::thread> th;
+  for (int b = 0; b < num_blocks; ++b)
+    if (!rows[b].empty()) {
+      if (n < (int64_t)1 << 16) block(b);  // small inputs: no thread start-up
+      else th.emplace_back(block, b);
+    }
+  for (auto& t : th) t.join();
 }
 
 // Contiguous shards of [0, n) balanced by nnz (ptr = CSR row pointer of the side, n + 1 entries).

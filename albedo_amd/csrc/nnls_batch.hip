@@ -70,8 +70,8 @@ struct NBatch {
   static constexpr int AS = KP + 4;                          // A·lastDir row stride (banks)
   static constexpr int OFF_A = OFF_U + SV * DLP;             // [SV][AS]: A·lastDir per slot (fp32)
   static constexpr int OFF_R = (OFF_A + SV * AS + 3) & ~3;   // doubles [2][NW][16][8]
-  static constexpr int OFF_C = OFF_R + 2 * 2 * NW * S * 8;      // ints
-  static constexpr int FLOATS = OFF_C + 4;
+  static constexpr int OFF_C = OFF_R + 2 * 2 * NW * S * 8;      // ints: [0] refill base, [4 + j] slot j's row
+  static constexpr int FLOATS = OFF_C + 4 + S;
   static_assert(NW * RBW == NQ && NQ % 2 == 0 && RBW <= 2, "row blocks split evenly over the waves");
   static_assert(DL >= 1 && FLOATS * 4 <= 160 * 1024, "LDS");
 };
@@ -323,7 +323,10 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
   double x[RBW][4], ax[RBW][4], ld[RBW][4];
   float bb[RBW][4];
   bool act = false;
-  int row = 0, iterno = 0, last_wall = 0, npos = 0, dd = 0;
+  // (the slot's row lives in LDS, ctl[4 + j], and its λn in one register: the loop is at the 256-VGPR
+  // budget, and every register freed there is a spill less)
+  int iterno = 0, last_wall = 0;
+  float lamn = 0.f;
   double last_norm = 0.0, hit = 0.0, last_dad = 0.0;
   const int iter_max = 400 > 20 * a.kreal ? 400 : 20 * a.kreal;
   bool exhausted = false;
@@ -352,11 +355,12 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
         const int64_t r = base + __popc(idle & ((1u << j) - 1u));
         if (r < a.n_rows) {
           act = true;
-          row = a.rows[r];
+          const int row = a.rows[r];
+          if (w == 0 && g == 0) ctl[4 + j] = row;
           const int64_t p0 = a.ptr[row];
-          dd = (int)(a.ptr[row + 1] - p0);
+          const int dd = (int)(a.ptr[row + 1] - p0);
           if (dd > DL) atomicOr(a.err, 4);  // host bucketing guarantees d <= DL
-          npos = 0;
+          int npos = 0;
 #pragma unroll
           for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
@@ -388,6 +392,7 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
             }
 #pragma unroll
           for (int rb = 0; rb < RBW; ++rb) *reinterpret_cast<f32x4*>(Aj + 16 * (w * RBW + rb) + 4 * g) = zero4();
+          lamn = a.reg * (float)(a.implicit ? npos : dd);
           iterno = 0;
           last_wall = 0;
           last_norm = 0.0;
@@ -399,7 +404,6 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
     }
     BT_PH(0);
     if ((__ballot(slot_lane && act) & ((1u << SV) - 1u)) == 0) break;  // drained (implies exhausted)
-    const float lamn = a.reg * (float)(a.implicit ? npos : dd);
 
     // ---- exact residual refresh (A·x) every 64 workgroup iterations -----------------------------
     if (wg_iter > 0 && (wg_iter & 63) == 0) {
@@ -545,7 +549,7 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
           o[t] = coord(rb, t) < a.kreal ? (float)x[rb][t] : 0.f;
           nonfinite |= !isfinite(o[t]);
         }
-        *reinterpret_cast<f32x4*>(a.X + (int64_t)row * KP + coord(rb, 0)) = f32x4{o[0], o[1], o[2], o[3]};
+        *reinterpret_cast<f32x4*>(a.X + (int64_t)ctl[4 + j] * KP + coord(rb, 0)) = f32x4{o[0], o[1], o[2], o[3]};
       }
       if (nonfinite) atomicOr(a.err, 2);
       if (a.iters && w == 0 && g == 0) {

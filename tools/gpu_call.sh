@@ -20,6 +20,8 @@ for s in "$@"; do
     bench_c2) timeout -k 10 300 python -u bench.py --config c2 --steps 10 --warmup 5 > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.err ;;
     bench_c5) timeout -k 10 400 python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err ;;
     prof_c4) timeout -k 10 1100 tools/prof.sh c4 r03 16384 > gpurun_out/prof_c4.log 2>&1 ;;
+    prof_c4r4) timeout -k 10 1100 tools/prof.sh c4 r04 16384 > gpurun_out/prof_c4r4.log 2>&1 ;;
+    prof_c5r4) timeout -k 10 900 tools/prof.sh c5 r04 0 > gpurun_out/prof_c5r4.log 2>&1 ;;
     prof_c5) timeout -k 10 900 tools/prof.sh c5 r03 0 > gpurun_out/prof_c5.log 2>&1 ;;
     prof_c2) timeout -k 10 600 tools/prof.sh c2 r03 16384 > gpurun_out/prof_c2.log 2>&1 ;;
     trace_c4) mkdir -p gpurun_out/trace_c4 && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_c4 -o run -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu --topk-users 16384 > gpurun_out/trace_c4/bench.json 2> gpurun_out/trace_c4/bench.err ;;
