@@ -182,6 +182,19 @@ def main():
         if found:
             traffic = float(sum(found))
 
+    # Gram / rotation matrix-core evidence: MFMA busy of the shipped kernels from the committed SQ
+    # counter passes of this config (tools/prof.sh -> tools/sqsum.py; PMC cannot run inside the bench)
+    mfma_evidence = None
+    spath = os.path.join(ROOT, "profiles", f"r04_{args.config}_sq_counters.json")
+    if os.path.exists(spath):
+        sj = json.load(open(spath))
+        mfma_evidence = {"source": os.path.relpath(spath, ROOT)}
+        for key, v in sj.items():
+            name = key.split("<")[0]
+            if name in ("gram_bf_kernel", "gram_partial_kernel", "rotate_bf_kernel", "rotate_kernel",
+                        "solve_wave_kernel", "topk_scan_kernel") and isinstance(v, dict) and "mfma_busy" in v:
+                mfma_evidence[key] = {"mfma_busy": v["mfma_busy"], "lds_conflict": v.get("lds_conflict")}
+
     # ---- top-30 users/s (secondary metric; a bounded user subset) ------------------------------
     # world > 1: every rank calls als_recommend (the users are sharded across the ranks, each scores
     # its slice against the replicated dst factors, the lists are all-gathered); timed between
@@ -258,6 +271,7 @@ def main():
                          "algorithmic_gb_per_sweep": d["bytes_per_sweep"] / 1e9,
                          "kernel_ms_per_sweep": d["ms"]},
             "cpu_baseline": cpu,
+            "mfma_busy_profiled": mfma_evidence,
             "topk30_users_per_s": topk_ups,
             "topk30": topk_info,
             "stages_ms_per_sweep": {f"{'user' if s == 0 else 'item'}_{n}": round((stage[s][i] / args.steps), 3)

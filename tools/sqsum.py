@@ -47,11 +47,14 @@ def main():
              "vgpr": a.get("_vgpr", b.get("_vgpr")), "lds_bytes": a.get("_lds", b.get("_lds"))}
         e.update({c: v for c, v in a.items() if not c.startswith("_")})
         e.update({c: v for c, v in b.items() if not c.startswith("_")})
-        cyc = b.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+        # GRBM_GUI_ACTIVE from whichever pass collected it (prof.sh: pass 2; pmc_topk4.sh: pass 1)
+        gp = b if "GRBM_GUI_ACTIVE" in b else a
+        cyc = gp.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
         if cyc and "SQ_VALU_MFMA_BUSY_CYCLES" in a:
             e["mfma_busy"] = a["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * 1024)
-        if cyc and d2.get(k):
-            e["clock_ghz"] = cyc / d2[k] * 1e-9
+        dur = (d2 if gp is b else d1).get(k)
+        if cyc and dur:
+            e["clock_ghz"] = cyc / dur * 1e-9
         w = a.get("SQ_WAVE_CYCLES")
         if w:
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
