@@ -14,8 +14,33 @@ import json
 import sys
 
 
+def demangle(name):
+    if not name.startswith("_Z"):
+        return name
+    import shutil
+    import subprocess
+    tool = shutil.which("c++filt") or "/opt/rocm/lib/llvm/bin/llvm-cxxfilt"
+    try:
+        return subprocess.run([tool, name], capture_output=True, text=True).stdout.strip() or name
+    except OSError:
+        return name
+
+
 def short(name):
-    k = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("albedo::", "")
+    k = demangle(name)
+    if k.startswith("_Z"):  # c++filt cannot read some (bf16 / fp16 parameter) manglings: name<int arg>
+        import re
+        i, last = 3 if k.startswith("_ZN") else 2, None  # <length><identifier> components
+        while i < len(k) and k[i].isdigit():
+            j = i
+            while k[j].isdigit():
+                j += 1
+            n = int(k[i:j])
+            last, i = k[j:j + n], j + n
+        m = re.match(r"ILi(\d+)E", k[i:])
+        if last:
+            return last + (f"<{m.group(1)}>" if m else "")
+    k = k.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("albedo::", "")
     return k.replace(" ", "")
 
 
