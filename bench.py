@@ -189,6 +189,13 @@ def main():
     if os.path.exists(spath):
         sj = json.load(open(spath))
         mfma_evidence = {"source": os.path.relpath(spath, ROOT)}
+        # the top-k scan's counters from the all-users profile when there is one (the sweep profile
+        # scores a 16K-user sample)
+        tkp = os.path.join(ROOT, "profiles", f"r04_{args.config}_topk_sq_counters.json")
+        if os.path.exists(tkp):
+            sj = {k: v for k, v in sj.items() if not k.startswith("topk_scan_kernel")}
+            sj.update({k: v for k, v in json.load(open(tkp)).items() if k.startswith("topk_scan_kernel")})
+            mfma_evidence["source_topk"] = os.path.relpath(tkp, ROOT)
         for key, v in sj.items():
             name = key.split("<")[0]
             if name in ("gram_bf_kernel", "gram_partial_kernel", "rotate_bf_kernel", "rotate_kernel",
