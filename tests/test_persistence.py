@@ -157,3 +157,31 @@ def test_builder_cache_reports_spec_mismatch(tmp_path, capsys):
     assert capsys.readouterr().err == ""
     builder.load_raw_starring(400, 60, 2000, seed=3, path=path)
     assert "using the existing starring data" in capsys.readouterr().err
+
+
+def test_starring_parallel_parts_match_serial(tmp_path):
+    """read_starring decodes uniform parts in parallel straight into preallocated columns and
+    write_starring encodes parts on a thread pool: the result equals the serial write / per-part
+    read + concatenation, in part order."""
+    import pyarrow.parquet as pq
+    rng = np.random.default_rng(7)
+    n = 10_000
+    stars = {"user_id": rng.integers(0, 500, n).astype(np.int32), "repo_id": rng.integers(0, 90, n).astype(np.int32),
+             "starred_at": (1_400_000_000 + rng.integers(0, 10**6, n)).astype("datetime64[s]"),
+             "starring": np.ones(n)}
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    seen = []
+    P.write_starring(a, stars, rows_per_part=777, workers=4, progress=lambda d, t: seen.append((d, t)))
+    P.write_starring(b, stars, rows_per_part=777)
+    assert seen[-1] == (13, 13)
+    ra, rb = P.read_starring(a), P.read_starring(b)
+    for c in P.STARRING_COLUMNS:
+        assert np.array_equal(ra[c], rb[c]) and np.array_equal(ra[c], np.asarray(stars[c]).astype(ra[c].dtype))
+    # a part with another schema (int64 ids) falls back to the per-part read + numpy promotion
+    t = pq.read_table(os.path.join(a, sorted(f for f in os.listdir(a) if f.endswith(".parquet"))[0]))
+    import pyarrow as pa
+    t2 = t.set_column(0, "user_id", pa.array(t.column("user_id").to_numpy().astype(np.int64)))
+    pq.write_table(t2, os.path.join(a, "part-99999-x-c000.snappy.parquet"), use_deprecated_int96_timestamps=True)
+    rc = P.read_starring(a)
+    assert rc["user_id"].dtype == np.int64 and rc["user_id"].size == n + t.num_rows
+    assert np.array_equal(rc["user_id"][:n], stars["user_id"])
