@@ -1769,9 +1769,63 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   const int64_t per_rank = (n_known + c->world - 1) / c->world;
   const int64_t lo = std::min<int64_t>(n_known, (int64_t)c->rank * per_rank);
   const int64_t hi = std::min<int64_t>(n_known, lo + per_rank);
+  // dense output (every row of the side, the recommendForAll* case): the caller's arrays are pinned
+  // in place and each pass's lists go down on a copy stream while the next pass computes (two device
+  // buffers); elsewise (or if pinning fails) each pass is copied back before the next starts
+  bool async_out = false;
+  hipStream_t cs = nullptr;
+  hipEvent_t ev_comp[2] = {nullptr, nullptr}, ev_copy[2] = {nullptr, nullptr};
+  DevBuf d_oid2[2], d_osc2[2];
+  if (dense_out && hi > lo && hi - lo > chunk) {
+    const size_t bytes = (size_t)(hi - lo) * k * 4;
+    if (hipHostRegister(dst_ids_out + lo * k, bytes, hipHostRegisterDefault) == hipSuccess) {
+      if (hipHostRegister(scores_out + lo * k, bytes, hipHostRegisterDefault) == hipSuccess) async_out = true;
+      else (void)hipHostUnregister(dst_ids_out + lo * k);
+    }
+    (void)hipGetLastError();  // a refused registration is not an error: the synchronous path runs
+    if (async_out) {
+      HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+      for (int b = 0; b < 2; ++b) {
+        HIPCHK(hipEventCreateWithFlags(&ev_comp[b], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ev_copy[b], hipEventDisableTiming));
+      }
+    }
+  }
+  auto end_async = [&]() {
+    if (!async_out) return;
+    (void)hipStreamSynchronize(cs);
+    (void)hipStreamSynchronize(c->st);
+    (void)hipHostUnregister(dst_ids_out + lo * k);
+    (void)hipHostUnregister(scores_out + lo * k);
+    for (int b = 0; b < 2; ++b) {
+      (void)hipEventDestroy(ev_comp[b]);
+      (void)hipEventDestroy(ev_copy[b]);
+    }
+    (void)hipStreamDestroy(cs);
+    async_out = false;
+  };
   DevBuf d_oid, d_osc;
-  for (int64_t q0 = lo; q0 < hi; q0 += chunk) {
+  for (int64_t q0 = lo, it = 0; q0 < hi; q0 += chunk, ++it) {
     const int64_t nc = std::min<int64_t>(chunk, hi - q0);
+    if (async_out) {
+      const int b = (int)(it & 1);
+      int rc = ALS_OK;
+      if (it >= 2 && hipStreamWaitEvent(c->st, ev_copy[b], 0) != hipSuccess) rc = fail(ALS_E_HIP, "stream wait");
+      if (rc == ALS_OK && (d_oid2[b].ensure(nc * k * 4) != hipSuccess || d_osc2[b].ensure(nc * k * 4) != hipSuccess))
+        rc = fail(ALS_E_OUT_OF_MEMORY, "top-k output buffers");
+      if (rc == ALS_OK) rc = topk_run_rows(c, P, known.data() + q0, nc, d_oid2[b].as<int32_t>(), d_osc2[b].as<float>());
+      if (rc == ALS_OK &&
+          (hipEventRecord(ev_comp[b], c->st) != hipSuccess || hipStreamWaitEvent(cs, ev_comp[b], 0) != hipSuccess ||
+           hipMemcpyAsync(dst_ids_out + q0 * k, d_oid2[b].p, nc * k * 4, hipMemcpyDeviceToHost, cs) != hipSuccess ||
+           hipMemcpyAsync(scores_out + q0 * k, d_osc2[b].p, nc * k * 4, hipMemcpyDeviceToHost, cs) != hipSuccess ||
+           hipEventRecord(ev_copy[b], cs) != hipSuccess))
+        rc = fail(ALS_E_HIP, "top-k result copy");
+      if (rc != ALS_OK) {
+        end_async();
+        return rc;
+      }
+      continue;
+    }
     HIPCHK(d_oid.ensure(nc * k * 4));
     HIPCHK(d_osc.ensure(nc * k * 4));
     TRYC(topk_run_rows(c, P, known.data() + q0, nc, d_oid.as<int32_t>(), d_osc.as<float>()));
@@ -1791,6 +1845,7 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
       }
     }
   }
+  end_async();
   if (c->world > 1 && per_rank > 0) {  // every rank ends with every list: one all-gather of the slices
     std::vector<float> blk((size_t)c->world * per_rank * k * 2, 0.f);
     float* mine = blk.data() + (size_t)c->rank * per_rank * k * 2;
