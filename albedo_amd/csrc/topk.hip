@@ -469,7 +469,13 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
   }
   wave_bitonic<NS>(s2, i2);
   const float t = rdlane(s2[0], a.kt - 1);  // the kt-th approximate score (-inf when fewer)
-  const int row = i2[0] >= 0 ? a.perm[i2[0]] : -1;
+  // Only the best kt candidates are rescored when the list can be certified (n_dst > TOPK_KC): a
+  // candidate ranked below kt has approx <= t, so its F2J score is <= t + e, and a certified row has
+  // its k-th exact score above t + e -- it cannot be in the top-k (nor tie).  A row that fails
+  // certification is re-scored by the exact scan from the k-th exact score of these kt (still a
+  // lower bound of the true k-th).  (Each rescored candidate reads a 512-B fp32 row from HBM.)
+  const bool rescore = a.n_dst <= TOPK_KC || lane < a.kt;
+  const int row = (i2[0] >= 0 && rescore) ? a.perm[i2[0]] : -1;
   float ex = -INFINITY;
   if (row >= 0) ex = f2j_dot_v4(s, a.T + (int64_t)row * KP, a.kreal);
   double nn = 0.0;
