@@ -182,6 +182,28 @@ def main():
         if found:
             traffic = float(sum(found))
 
+    # NNLS configs: the solve is iteration-latency bound (Spark's projected-gradient loop, hundreds of
+    # dependent iterations per row), so the roofline that means something is per row-iteration: the
+    # CU cycles one row-iteration takes (solve time x CUs x clock / row-iterations, the iteration
+    # counts of the last sweep) against the k^2 FMAs of its one product A.v at the CU's packed-fp32
+    # rate (512 FMA per cycle: 4 SIMDs x 64 lanes x v_pk_fma_f32)
+    latency_roofline = None
+    if args.config in NONNEGATIVE and nnls_iters:
+        n_cu, ghz = 256, 2.4
+        floor = k * k / 512.0
+        per = {}
+        lock_it = sum(nnls_iters[sd]["lockstep_mean"] * nnls_iters[sd]["lockstep_rows"] for sd in nnls_iters)
+        row_it = sum(nnls_iters[sd]["per_row_kernel_mean"] * (nnls_iters[sd]["rows"] - nnls_iters[sd]["lockstep_rows"])
+                     for sd in nnls_iters)
+        for name, ms, its in (("nnls_batch (lockstep)", kern["nnls_batch"]["ms"], lock_it),
+                              ("solve_nnls (per row)", kern["solve_nnls"]["ms"], row_it)):
+            if its > 0 and ms > 0:
+                cyc = ms / 1000.0 * n_cu * ghz * 1e9 / its
+                per[name] = {"cycles_per_row_iteration": cyc, "floor_cycles": floor, "frac": floor / cyc,
+                             "row_iterations": its, "ms_per_sweep": ms}
+        latency_roofline = {"bound": "latency (dependent iterations)", "unit": "CU cycles per row-iteration",
+                            "clock_ghz_assumed": ghz, "kernels": per}
+
     # Gram / rotation matrix-core evidence: MFMA busy of the shipped kernels from the committed SQ
     # counter passes of this config (tools/prof.sh -> tools/sqsum.py; PMC cannot run inside the bench)
     mfma_evidence = None
@@ -257,7 +279,10 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(lib, L, h, k, nnz, n_users, n_items, args.cpu_seconds)
+        if args.config in NONNEGATIVE:
+            cpu = cpu_baseline_nnls(lib, L, h, k, nnz, n_users, n_items, args.cpu_seconds)
+        else:
+            cpu = cpu_baseline(lib, L, h, k, nnz, n_users, n_items, args.cpu_seconds)
 
     if rank == 0:
         line = {
@@ -279,6 +304,7 @@ def main():
                          "kernel_ms_per_sweep": d["ms"]},
             "cpu_baseline": cpu,
             "mfma_busy_profiled": mfma_evidence,
+            "latency_roofline": latency_roofline,
             "topk30_users_per_s": topk_ups,
             "topk30": topk_info,
             "stages_ms_per_sweep": {f"{'user' if s == 0 else 'item'}_{n}": round((stage[s][i] / args.steps), 3)
@@ -401,6 +427,71 @@ def cpu_baseline(lib, L, h, k, nnz, n_users, n_items, budget_s):
             "sample": (f"fp64 C/OpenMP restatement of Spark's half-sweep (oracle/c/als_cpu.c, {threads} threads): "
                        f"full Gram of each src side + a degree-stratified row sample ({sampled} stars, strata "
                        f"{list(STRATA)}) solved, each stratum extrapolated by its own star count to one sweep")}
+
+
+def cpu_baseline_nnls(lib, L, h, k, nnz, n_users, n_items, budget_s):
+    """NNLS configs: the numpy fp64 restatement of Spark's NNLSSolver (oracle/spark_als.py nnls_solve,
+    one core: a row's projected-gradient loop is sequential) on a degree-stratified row sample; the
+    Gram of each src side by the C/OpenMP restatement.  A row's cost is its iteration count times a
+    k x k product, not its star count, so each stratum is extrapolated by its row count."""
+    from threadpoolctl import threadpool_limits
+    from oracle import cbind
+    from oracle import spark_als as O
+    info = host_cpu_info()
+    res, t_sweep = {}, 0.0
+    with threadpool_limits(limits=1):
+        for dst, n_dst, n_src in ((0, n_users, n_items), (1, n_items, n_users)):
+            src = 1 - dst
+            sids = np.empty(n_src, np.int32)
+            sf = np.empty((n_src, k), np.float32)
+            L.check(lib.als_get_factors(h, src, L.ptr(sids, C.c_int32), L.ptr(sf, C.c_float)))
+            t0 = time.perf_counter()
+            G = cbind.gram(sf, threads=info["usable"])
+            g_s = time.perf_counter() - t0
+            dids = np.empty(n_dst, np.int32)
+            L.check(lib.als_get_ids(h, dst, L.ptr(dids, C.c_int32)))
+            deg = np.empty(n_dst, np.int64)
+            L.check(lib.als_get_degrees(h, dst, L.ptr(deg, C.c_int64)))
+            rng = np.random.default_rng(11 + dst)
+            edges = list(STRATA) + [int(deg.max()) + 1]
+            n_b = sum(1 for a, b in zip(edges[:-1], edges[1:]) if np.any((deg >= a) & (deg < b)))
+            strata, t_side = [], g_s
+            n_row = np.empty(1, np.int64)
+            for a, b in zip(edges[:-1], edges[1:]):
+                rows = np.nonzero((deg >= a) & (deg < b))[0]
+                if rows.size == 0:
+                    continue
+                order = rng.permutation(rows)
+                done, t_rows = 0, 0.0
+                while done < order.size and (t_rows < budget_s / (2 * n_b) or done == 0) and done < 4096:
+                    r = order[done]
+                    done += 1
+                    m = int(deg[r])
+                    bi, bv = np.empty(max(m, 1), np.int32), np.empty(max(m, 1), np.float32)
+                    L.check(lib.als_get_row_ratings(h, dst, int(dids[r]), m, L.ptr(bi, C.c_int32),
+                                                    L.ptr(bv, C.c_float), L.ptr(n_row, C.c_int64)))
+                    Y = sf[np.searchsorted(sids, bi[:m])].astype(np.float64)
+                    rv = bv[:m].astype(np.float64)
+                    t1 = time.perf_counter()
+                    c = 40.0 * np.abs(rv)
+                    A = G + (Y.T * c) @ Y
+                    bvec = Y.T @ np.where(rv > 0, 1.0 + c, 0.0)
+                    O.nnls_solve(A, bvec, 0.5 * float(np.sum(rv > 0)))
+                    t_rows += time.perf_counter() - t1
+                est = t_rows * rows.size / done
+                strata.append(dict(lo=a, rows=int(rows.size), sampled_rows=int(done), s=est))
+                t_side += est
+            res[dst] = dict(gram_s=g_s, strata=strata, side_s=t_side)
+            t_sweep += t_side
+            del sf
+    sampled = sum(st["sampled_rows"] for d in res for st in res[d]["strata"])
+    return {"value": nnz / t_sweep, "unit": "interactions/s", "cores": 1, "kind": "port",
+            "host": {k2: info[k2] for k2 in ("nproc", "affinity", "cgroup_quota", "model")},
+            "sweep_s_extrapolated": t_sweep,
+            "strata": {("user" if d == 0 else "item"): res[d]["strata"] for d in res},
+            "sample": (f"numpy fp64 restatement of Spark's NNLSSolver (oracle/spark_als.py nnls_solve, one core) on "
+                       f"{sampled} degree-stratified rows (strata {list(STRATA)}), each stratum extrapolated by its "
+                       f"row count; the Gram by the C/OpenMP restatement ({info['usable']} threads)")}
 
 
 if __name__ == "__main__":
