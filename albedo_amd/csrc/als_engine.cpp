@@ -379,14 +379,12 @@ int rank_layout(als_ctx* c) {
     all.reserve(S.own_n);
     for (int b = 0; b < NBUCKET; ++b) {
       S.boff[b] = (int64_t)all.size();
-      // grouped by solve chunk; B_L16: within a chunk by ascending degree (light16 pairs the rows of
-      // degree <= 8, and a unit's code is specialised on its degree bound: neighbouring waves then run
-      // the same instantiation)
+      // grouped by solve chunk; B_L16: within a chunk the rows of degree <= 8 first (light16 pairs them)
       const bool pairs = b == B_L16;
       std::stable_sort(rows[b].begin(), rows[b].end(), [&](int32_t x, int32_t y) {
         const int cx = chunk_of(x), cy = chunk_of(y);
         if (cx != cy || !pairs) return cx < cy;
-        return S.h_deg[x] < S.h_deg[y];
+        return (S.h_deg[x] <= 8) > (S.h_deg[y] <= 8);
       });
       int64_t p = 0;
       for (int q = 0; q <= nsolve; ++q) {

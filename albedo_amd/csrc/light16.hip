@@ -71,11 +71,7 @@ __device__ __forceinline__ bool entry_valid(const SolveArgs& a, float r, int i16
 // the Cholesky steps and the x' stage: K is block diagonal (the cross block is zeroed), so the
 // factorisation of one block never touches the other (L's cross entries stay exactly 0), and each
 // row's arithmetic is the one it would get alone.
-// columns a unit of bound DM walks: PAIR: 0..DM-1 of each 8-entry block; single: 0..DM-1
-template <bool PAIR, int DM>
-__device__ __forceinline__ constexpr bool l16_live(int c) { return PAIR ? (c & 7) < DM : c < DM; }
-
-template <int KP, bool PAIR, int DM>
+template <int KP, bool PAIR>
 __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB, float r, int colE,
                                              const f32x4 (&zf)[KP / 16], float* st, float* sdlA, float* sdlB,
                                              float* vsh, const float* s_lam, const float* s_csi,
@@ -158,10 +154,8 @@ __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB,
 #pragma unroll
     for (int e = 0; e < 4; ++e) kr[4 * u + e] = v[e];
   }
-  // DM (compile time) bounds the degrees of the unit's rows: the Cholesky and both substitutions
-  // walk the columns c < DM of each block with no per-column tests.  A column at or past its own
-  // row's degree is an identity row (K[c][c] = 1, zero off the diagonal: its entry gathered the
-  // zero row) with right-hand side 0, so its step leaves every value unchanged (exact: x·1, x − 0)
+  // live column c: an entry of its row (c < dA, or PAIR: block B's c - 8 < dB)
+  auto live = [&](int c) { return PAIR ? (c < 8 ? c < dA : c - 8 < dB) : c < dA; };
 
   // Cholesky K = L Lᵀ over the live columns (lane i holds row i: kr[m] = L[i][m], m <= i), with the
   // forward substitution L y = C⁻¹ w in the same steps; broadcasts of lane c by DPP row_newbcast
@@ -170,8 +164,7 @@ __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB,
   static_for<0, 16>([&](auto cc) {
     constexpr int c = decltype(cc)::value;
     constexpr int cend = (PAIR && c < 8) ? 8 : 16;  // PAIR: the other block's rows are untouched
-    if constexpr (!l16_live<PAIR, DM>(c)) return;
-    else {
+    if (!live(c)) return;
     const float piv = bc16_after_asm<c>(kr[c]);
     if (!(piv > 0.f)) notpd = true;
     const float inv = frsq(piv), s = piv * inv;
@@ -179,11 +172,11 @@ __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB,
     dg = (i16 == c) ? inv : dg;
     static_for<c + 1, cend>([&](auto mm) {
       constexpr int m = decltype(mm)::value;
-      if constexpr (l16_live<PAIR, DM>(m)) fnmac_bc16<m, m == c + 1>(kr[m], kr[c], kr[c]);
+      if (!live(m)) return;
+      fnmac_bc16<m, m == c + 1>(kr[m], kr[c], kr[c]);
     });
     const float yc = bc16<c>(y * dg);
     y = (i16 > c) ? fmaf(-kr[c], yc, y) : ((i16 == c) ? yc : y);
-    }
   });
   if (notpd && lane == 0) atomicOr(a.err, 2 | ALBEDO_EF_LIGHT16);
   // Lᵀ v = y: lane i needs column i of L (transposed through the scratch)
@@ -198,18 +191,17 @@ __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB,
   for (int m = 0; m < 16; ++m) lt[m] = st[m * L16_LDK + i16];  // L[m][i16] (m >= i16 used)
   static_for<0, 16>([&](auto cc) {
     constexpr int c = 15 - decltype(cc)::value;
-    if constexpr (l16_live<PAIR, DM>(c)) {
-      const float vc = bc16<c>(y * dg);
-      y = (i16 < c) ? fmaf(-lt[c], vc, y) : ((i16 == c) ? vc : y);
-    }
+    if (!live(c)) return;
+    const float vc = bc16<c>(y * dg);
+    y = (i16 < c) ? fmaf(-lt[c], vc, y) : ((i16 == c) ? vc : y);
   });
   if (g == 0) vsh[i16] = y;  // v (zero for masked / absent entries)
 
   // x' = D⁻¹ Zᵀ v through the stage: 64 columns per pass; lane l sums columns 2(l & 31), +1 over the
   // entries 8(l >> 5) + u.  Single row: u < min(8, d), the two halves meet by one cross-half shuffle;
-  // PAIR: half 0 is row A, half 1 row B (u < DM: absent entries are zero rows with v = 0).
+  // PAIR: half 0 is row A, half 1 row B (u < max(dA, dB): absent entries are zero rows with v = 0).
   const int eh = lane >> 5, cl = 2 * (lane & 31);
-  constexpr int nu = PAIR ? DM : (DM < 8 ? DM : 8);  // entries per half (zero rows past a row's degree add 0)
+  const int nu = PAIR ? (dA > dB ? dA : dB) : (dA < 8 ? dA : 8);
   const float* sdo = (PAIR && eh) ? sdlB : sdlA;
 #pragma unroll
   for (int h = 0; h < KP / L16_COLS; ++h) {
@@ -219,7 +211,6 @@ __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB,
       *reinterpret_cast<f32x4*>(st + i16 * L16_SLD + 16 * c4 + 4 * g) = zf[4 * h + c4];
     WAVE_LDS_SYNC();
     f32x2 xa = {0.f, 0.f};
-#pragma unroll
     for (int u = 0; u < nu; ++u) {
       const int e = 8 * eh + u;
       const f32x2 z2 = *reinterpret_cast<const f32x2*>(st + e * L16_SLD + cl);
@@ -311,35 +302,7 @@ __global__ __launch_bounds__(256, KP <= 128 ? 5 : 4) void solve_light16_kernel(S
   Unit uC = unit(uidx + 2 * nw);
   for (;;) {
     f32x2 xo[KP / L16_COLS];
-    // the row list is sorted by degree, so the waves of a CU run the same instantiation together
-    auto run = [&](auto dm) {
-      light16_unit<KP, PAIR, decltype(dm)::value>(a, uA.a.w, uA.b.w, r, colE, zf, st, sdlA, sdlB, vsh, s_lam, s_csi, xo);
-    };
-    using std::integral_constant;
-    const int dmax = PAIR ? (uA.a.w > uA.b.w ? uA.a.w : uA.b.w) : uA.a.w;  // wave-uniform (scalar loads)
-    if constexpr (PAIR) {
-      switch (dmax) {
-        case 0: case 1: run(integral_constant<int, 1>{}); break;
-        case 2: run(integral_constant<int, 2>{}); break;
-        case 3: run(integral_constant<int, 3>{}); break;
-        case 4: run(integral_constant<int, 4>{}); break;
-        case 5: run(integral_constant<int, 5>{}); break;
-        case 6: run(integral_constant<int, 6>{}); break;
-        case 7: run(integral_constant<int, 7>{}); break;
-        default: run(integral_constant<int, 8>{}); break;
-      }
-    } else {
-      switch (dmax) {
-        case 9: run(integral_constant<int, 9>{}); break;
-        case 10: run(integral_constant<int, 10>{}); break;
-        case 11: run(integral_constant<int, 11>{}); break;
-        case 12: run(integral_constant<int, 12>{}); break;
-        case 13: run(integral_constant<int, 13>{}); break;
-        case 14: run(integral_constant<int, 14>{}); break;
-        case 15: run(integral_constant<int, 15>{}); break;
-        default: run(integral_constant<int, 16>{}); break;
-      }
-    }
+    light16_unit<KP, PAIR>(a, uA.a.w, uA.b.w, r, colE, zf, st, sdlA, sdlB, vsh, s_lam, s_csi, xo);
     const Unit done = uA;
     uidx += nw;
     if (uidx >= nu_) {

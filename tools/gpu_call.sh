@@ -50,6 +50,7 @@ for s in "$@"; do
       { timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err; r=$?; cp /tmp/albedo_main.so albedo_amd/libalbedo_als.so; [ $r -eq 0 ]; } ;;
     debug_eig) timeout -k 10 600 python -u tools/debug_eig.py > gpurun_out/debug_eig.log 2>&1; r=$?; echo "debug_eig rc $r"; [ $r -le 1 ] ;;
     debug_c1) timeout -k 10 300 python -u tools/debug_c1.py > gpurun_out/debug_c1.log 2>&1; r=$?; echo "debug_c1 rc $r"; [ $r -le 1 ] ;;
+    protocol_eu) { timeout -k 10 300 python -u tools/protocol_eu.py main; } > gpurun_out/protocol_eu.log 2>&1 ;;
     factortime)(cd tools/probe && timeout -k 5 120 ./factortime 1000000) > gpurun_out/factortime.txt 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
