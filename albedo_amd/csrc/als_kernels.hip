@@ -544,22 +544,37 @@ __global__ __launch_bounds__(64 * RBF_WAVES) void rotate_bf_kernel(const float* 
     // output rows: lane l writes row r0 + (l >> 2), columns 16J + 4(l & 3) .. +3
     const int orow = lane >> 2, oc = 4 * (lane & 3);
     const int64_t rr = r0 + orow;
-#pragma unroll 2
-    for (int J = 0; J < NJ; ++J) {
-      f32x4 acc = zero4();
+    // two column blocks per step: their accumulator chains interleave (each chain keeps its own
+    // product order, so Z is bit-identical to one block at a time)
+    for (int J2 = 0; J2 < NJ; J2 += 2) {
+      f32x4 acc2[2] = {zero4(), zero4()};
 #pragma unroll
       for (int kc = 0; kc < NK; ++kc) {
-        const __bf16* pf = sPf + ((J * NK + kc) * 3) * 512 + lane * 8;
-        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(pf);
-        const bf16x8 bm = *reinterpret_cast<const bf16x8*>(pf + 512);
-        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(pf + 1024);
-        acc = mfma_b(al[kc], bh, acc);  // the small terms first
-        acc = mfma_b(ah[kc], bl, acc);
-        acc = mfma_b(am[kc], bm, acc);
-        acc = mfma_b(am[kc], bh, acc);
-        acc = mfma_b(ah[kc], bm, acc);
-        acc = mfma_b(ah[kc], bh, acc);
+        bf16x8 bh[2], bm[2], bl[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const __bf16* pf = sPf + (((J2 + u) * NK + kc) * 3) * 512 + lane * 8;
+          bh[u] = *reinterpret_cast<const bf16x8*>(pf);
+          bm[u] = *reinterpret_cast<const bf16x8*>(pf + 512);
+          bl[u] = *reinterpret_cast<const bf16x8*>(pf + 1024);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc2[u] = mfma_b(al[kc], bh[u], acc2[u]);  // the small terms first
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc2[u] = mfma_b(ah[kc], bl[u], acc2[u]);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc2[u] = mfma_b(am[kc], bm[u], acc2[u]);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc2[u] = mfma_b(am[kc], bh[u], acc2[u]);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc2[u] = mfma_b(ah[kc], bm[u], acc2[u]);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc2[u] = mfma_b(ah[kc], bh[u], acc2[u]);
       }
+#pragma unroll
+     for (int u = 0; u < 2; ++u) {
+      const int J = J2 + u;
+      const f32x4 acc = acc2[u];
       // C layout (lane j + 16q: Z[r0 + 4q + r][16J + j]) -> LDS -> 16-B row pieces
 #pragma unroll
       for (int r = 0; r < 4; ++r) tsc[(4 * q + r) * RBF_TS + i16] = acc[r];
@@ -584,6 +599,7 @@ __global__ __launch_bounds__(64 * RBF_WAVES) void rotate_bf_kernel(const float* 
           *reinterpret_cast<f16x4*>(Zhl + rr * 2 * KP + KP + c) = l4;
         }
       }
+     }
     }
   }
 }
