@@ -458,6 +458,7 @@ __global__ void rotate_pfrag_kernel(const float* __restrict__ P, __bf16* __restr
 }
 
 constexpr int RBF_WAVES = 8, RBF_TS = 20;  // waves per block, transpose row stride (floats)
+constexpr int RBF_JU = 2;                  // column blocks whose accumulator chains interleave
 template <int KP>
 __global__ __launch_bounds__(64 * RBF_WAVES) void rotate_bf_kernel(const float* __restrict__ X, const __bf16* __restrict__ Pf,
                                                                   float* __restrict__ Z, int64_t n, const float* __restrict__ cs,
@@ -544,35 +545,37 @@ __global__ __launch_bounds__(64 * RBF_WAVES) void rotate_bf_kernel(const float* 
     // output rows: lane l writes row r0 + (l >> 2), columns 16J + 4(l & 3) .. +3
     const int orow = lane >> 2, oc = 4 * (lane & 3);
     const int64_t rr = r0 + orow;
-    // two column blocks per step: their accumulator chains interleave (each chain keeps its own
+    // RBF_JU column blocks per step: their accumulator chains interleave (each chain keeps its own
     // product order, so Z is bit-identical to one block at a time)
-    for (int J2 = 0; J2 < NJ; J2 += 2) {
-      f32x4 acc2[2] = {zero4(), zero4()};
+    for (int J2 = 0; J2 < NJ; J2 += RBF_JU) {
+      f32x4 acc2[RBF_JU];
+#pragma unroll
+      for (int u = 0; u < RBF_JU; ++u) acc2[u] = zero4();
 #pragma unroll
       for (int kc = 0; kc < NK; ++kc) {
-        bf16x8 bh[2], bm[2], bl[2];
+        bf16x8 bh[RBF_JU], bm[RBF_JU], bl[RBF_JU];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < RBF_JU; ++u) {
           const __bf16* pf = sPf + (((J2 + u) * NK + kc) * 3) * 512 + lane * 8;
           bh[u] = *reinterpret_cast<const bf16x8*>(pf);
           bm[u] = *reinterpret_cast<const bf16x8*>(pf + 512);
           bl[u] = *reinterpret_cast<const bf16x8*>(pf + 1024);
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) acc2[u] = mfma_b(al[kc], bh[u], acc2[u]);  // the small terms first
+        for (int u = 0; u < RBF_JU; ++u) acc2[u] = mfma_b(al[kc], bh[u], acc2[u]);  // the small terms first
 #pragma unroll
-        for (int u = 0; u < 2; ++u) acc2[u] = mfma_b(ah[kc], bl[u], acc2[u]);
+        for (int u = 0; u < RBF_JU; ++u) acc2[u] = mfma_b(ah[kc], bl[u], acc2[u]);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) acc2[u] = mfma_b(am[kc], bm[u], acc2[u]);
+        for (int u = 0; u < RBF_JU; ++u) acc2[u] = mfma_b(am[kc], bm[u], acc2[u]);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) acc2[u] = mfma_b(am[kc], bh[u], acc2[u]);
+        for (int u = 0; u < RBF_JU; ++u) acc2[u] = mfma_b(am[kc], bh[u], acc2[u]);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) acc2[u] = mfma_b(ah[kc], bm[u], acc2[u]);
+        for (int u = 0; u < RBF_JU; ++u) acc2[u] = mfma_b(ah[kc], bm[u], acc2[u]);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) acc2[u] = mfma_b(ah[kc], bh[u], acc2[u]);
+        for (int u = 0; u < RBF_JU; ++u) acc2[u] = mfma_b(ah[kc], bh[u], acc2[u]);
       }
 #pragma unroll
-     for (int u = 0; u < 2; ++u) {
+     for (int u = 0; u < RBF_JU; ++u) {
       const int J = J2 + u;
       const f32x4 acc = acc2[u];
       // C layout (lane j + 16q: Z[r0 + 4q + r][16J + j]) -> LDS -> 16-B row pieces
