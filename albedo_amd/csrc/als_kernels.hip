@@ -458,7 +458,7 @@ __global__ void rotate_pfrag_kernel(const float* __restrict__ P, __bf16* __restr
 }
 
 constexpr int RBF_WAVES = 8, RBF_TS = 20;  // waves per block, transpose row stride (floats)
-constexpr int RBF_JU = 2;                  // column blocks whose accumulator chains interleave
+constexpr int RBF_JU = 4;                  // column blocks whose accumulator chains interleave
 template <int KP>
 __global__ __launch_bounds__(64 * RBF_WAVES) void rotate_bf_kernel(const float* __restrict__ X, const __bf16* __restrict__ Pf,
                                                                   float* __restrict__ Z, int64_t n, const float* __restrict__ cs,
