@@ -990,6 +990,9 @@ int half_sweep(als_ctx* c, int t) {
     T.t[ALS_T_SOLVE_HEAVY] = event_ms(ev[5], ev[6]);
   }
   T.t[ALS_T_HALF_TOTAL] = event_ms(ev[0], ev[6]);
+  if (sweeps < 0)  // eig.hip: the Jacobi sweep budget ran out (the host eigensolver's "did not converge")
+    return fail(ALS_E_NOT_POSITIVE_DEFINITE, "eigensolver did not converge (device Jacobi: " +
+                                                 std::to_string(-sweeps - 1) + " sweeps without meeting the tolerance)");
   if (err & 3)
     return fail(ALS_E_NOT_POSITIVE_DEFINITE,
                 "LAPACK.dppsv-equivalent Cholesky met a non-positive pivot because A is not positive "
@@ -1783,27 +1786,36 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
       else (void)hipHostUnregister(dst_ids_out + lo * k);
     }
     (void)hipGetLastError();  // a refused registration is not an error: the synchronous path runs
-    if (async_out) {
-      HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
-      for (int b = 0; b < 2; ++b) {
-        HIPCHK(hipEventCreateWithFlags(&ev_comp[b], hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&ev_copy[b], hipEventDisableTiming));
-      }
-    }
   }
+  // releases everything the async path holds (null-safe: also after a partial set-up)
   auto end_async = [&]() {
     if (!async_out) return;
-    (void)hipStreamSynchronize(cs);
+    if (cs) (void)hipStreamSynchronize(cs);
     (void)hipStreamSynchronize(c->st);
     (void)hipHostUnregister(dst_ids_out + lo * k);
     (void)hipHostUnregister(scores_out + lo * k);
     for (int b = 0; b < 2; ++b) {
-      (void)hipEventDestroy(ev_comp[b]);
-      (void)hipEventDestroy(ev_copy[b]);
+      if (ev_comp[b]) (void)hipEventDestroy(ev_comp[b]);
+      if (ev_copy[b]) (void)hipEventDestroy(ev_copy[b]);
+      ev_comp[b] = ev_copy[b] = nullptr;
     }
-    (void)hipStreamDestroy(cs);
+    if (cs) (void)hipStreamDestroy(cs);
+    cs = nullptr;
     async_out = false;
   };
+  if (async_out) {  // the copy stream and its events; if any cannot be created, the synchronous path runs
+    bool ok = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) == hipSuccess;
+    if (!ok) cs = nullptr;
+    for (int b = 0; b < 2 && ok; ++b) {
+      ok = hipEventCreateWithFlags(&ev_comp[b], hipEventDisableTiming) == hipSuccess;
+      if (!ok) ev_comp[b] = nullptr;
+      else if (!(ok = hipEventCreateWithFlags(&ev_copy[b], hipEventDisableTiming) == hipSuccess)) ev_copy[b] = nullptr;
+    }
+    if (!ok) {
+      end_async();
+      (void)hipGetLastError();
+    }
+  }
   DevBuf d_oid, d_osc;
   for (int64_t q0 = lo, it = 0; q0 < hi; q0 += chunk, ++it) {
     const int64_t nc = std::min<int64_t>(chunk, hi - q0);
@@ -2158,7 +2170,8 @@ int als_device_eigh(int32_t device, int32_t k, const double* g, const double* w0
     w[i] = wk[i];
     for (int j = 0; j < k; ++j) v[(size_t)i * k + j] = P[(size_t)i * KP + j];
   }
-  if (sweeps) *sweeps = sw;
+  if (sweeps) *sweeps = sw < 0 ? -sw - 1 : sw;
+  if (sw < 0) return fail(ALS_E_NOT_POSITIVE_DEFINITE, "eigensolver did not converge");
   return ALS_OK;
 }
 

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
+#include <algorithm>
 #include "device_common.h"
 #include "kernels.h"
 
@@ -36,7 +38,16 @@ __global__ __launch_bounds__(256) void dgemm_kp_kernel(const double* __restrict_
 }
 
 constexpr int JAC_THREADS = 1024;
+// Sweep budget.  A run that spends it without meeting the tolerance below reports a negative sweep
+// count (-(sweeps + 1)), and the engine fails the half-sweep as the host eigensolver it replaced did
+// (ALS_E_NOT_POSITIVE_DEFINITE, "did not converge"): the light push-through solves assume Λ is the
+// diagonal of the Gram in the basis P.  ALBEDO_JAC_MAX_SWEEPS lowers the budget (test knob).
 constexpr int JAC_MAX_SWEEPS = 30;
+int jacobi_max_sweeps() {
+  const char* e = std::getenv("ALBEDO_JAC_MAX_SWEEPS");
+  if (e && *e) return std::max(0, std::min(JAC_MAX_SWEEPS, std::atoi(e)));
+  return JAC_MAX_SWEEPS;
+}
 // Convergence: off-diagonal mass <= 1e-28 of the diagonal's (off-diagonal norm 1e-14 of the diagonal's,
 // about fp64 rounding at k <= 256: a backward error of the order of a Householder + QL solve).  The
 // small eigenpairs need it: at 1e-9 the directions of eigenvalues near 1e-9·‖G‖ keep components of the
@@ -63,7 +74,8 @@ __device__ __forceinline__ void rr_pair(int r, int i, int n, int& a, int& b) {
 // workgroup's own stores, ordered by its barriers).
 template <bool LDSM>
 __global__ __launch_bounds__(JAC_THREADS) void jacobi_kernel(double* __restrict__ Mg, double* __restrict__ VT,
-                                                             double* __restrict__ w, int k, int KP, int* __restrict__ sweeps_out) {
+                                                             double* __restrict__ w, int k, int KP, int max_sweeps,
+                                                             int* __restrict__ sweeps_out) {
   extern __shared__ double sm[];
   __shared__ double cs[2 * 128];  // c, s of the round's pairs (k <= 256: at most 128 pairs)
   __shared__ int pq[2 * 128];     // p, q
@@ -79,7 +91,7 @@ __global__ __launch_bounds__(JAC_THREADS) void jacobi_kernel(double* __restrict_
   const int np = n / 2;
   __syncthreads();
   int sweep = 0;
-  for (; sweep < JAC_MAX_SWEEPS; ++sweep) {
+  for (;; ++sweep) {
     // convergence: off-diagonal mass against the diagonal's (fixed-order block reduction)
     double off = 0.0, dia = 0.0;
     for (int e = tid; e < k * k; e += JAC_THREADS) {
@@ -104,6 +116,7 @@ __global__ __launch_bounds__(JAC_THREADS) void jacobi_kernel(double* __restrict_
         sd += red[i][1];
       }
       done = !(so > JAC_TOL * sd) || (!(so > 1e-20 * sd) && !(so < 0.5 * prev_off));  // or at the rounding floor
+      if (!done && sweep >= max_sweeps) done = 2;  // the sweep budget is spent: not converged
       prev_off = so;
     }
     __syncthreads();
@@ -162,7 +175,7 @@ __global__ __launch_bounds__(JAC_THREADS) void jacobi_kernel(double* __restrict_
     }
   }
   for (int i = tid; i < KP; i += JAC_THREADS) w[i] = i < k ? M[i * ld + i] : 0.0;
-  if (tid == 0 && sweeps_out) *sweeps_out = sweep;
+  if (tid == 0 && sweeps_out) *sweeps_out = done == 2 ? -sweep - 1 : sweep;  // < 0: did not converge
 }
 
 // k <= 128: JAC_WG workgroups sweep identical copies of M in LDS (same code, same inputs, fixed
@@ -172,7 +185,7 @@ __global__ __launch_bounds__(JAC_THREADS) void jacobi_kernel(double* __restrict_
 // pair b's columns: both sides of the similarity in one pass) and VT's rows, a barrier.
 constexpr int JAC_WG = 8;
 __global__ __launch_bounds__(JAC_THREADS) void jacobi_lds_kernel(const double* __restrict__ Mg, double* __restrict__ VTg,
-                                                                 double* __restrict__ w, int k, int KP,
+                                                                 double* __restrict__ w, int k, int KP, int max_sweeps,
                                                                  int* __restrict__ sweeps_out) {
   extern __shared__ double sm[];
   __shared__ double cs[2 * 64];
@@ -192,7 +205,7 @@ __global__ __launch_bounds__(JAC_THREADS) void jacobi_lds_kernel(const double* _
   const int np = n / 2;
   __syncthreads();
   int sweep = 0;
-  for (; sweep < JAC_MAX_SWEEPS; ++sweep) {
+  for (;; ++sweep) {
     double off = 0.0, dia = 0.0;
     for (int e = tid; e < k * k; e += JAC_THREADS) {
       const int i = e / k, j = e % k;
@@ -216,6 +229,7 @@ __global__ __launch_bounds__(JAC_THREADS) void jacobi_lds_kernel(const double* _
         sd += red[i][1];
       }
       done = !(so > JAC_TOL * sd) || (!(so > 1e-20 * sd) && !(so < 0.5 * prev_off));  // or at the rounding floor
+      if (!done && sweep >= max_sweeps) done = 2;  // the sweep budget is spent: not converged
       prev_off = so;
     }
     __syncthreads();
@@ -275,7 +289,7 @@ __global__ __launch_bounds__(JAC_THREADS) void jacobi_lds_kernel(const double* _
   for (int e = tid; e < KP * nc; e += JAC_THREADS) VTg[(e / nc) * KP + c0 + e % nc] = VT[e];
   if (blockIdx.x == 0) {
     for (int i = tid; i < KP; i += JAC_THREADS) w[i] = i < k ? M[i * ld + i] : 0.0;
-    if (tid == 0 && sweeps_out) *sweeps_out = sweep;
+    if (tid == 0 && sweeps_out) *sweeps_out = done == 2 ? -sweep - 1 : sweep;  // < 0: did not converge
   }
 }
 
@@ -353,9 +367,9 @@ hipError_t launch_device_eig(int KP, int k, const double* G, const double* Bs, c
     const size_t lds = ((size_t)k * (k + 1) + (size_t)KP * (KP / JAC_WG)) * sizeof(double);
     static const hipError_t attr = allow_lds(jacobi_lds_kernel, ((size_t)128 * 129 + 128 * 16) * 8);
     if (attr != hipSuccess) return attr;
-    jacobi_lds_kernel<<<JAC_WG, JAC_THREADS, lds, s>>>(M, WT, w, k, KP, sweeps);
+    jacobi_lds_kernel<<<JAC_WG, JAC_THREADS, lds, s>>>(M, WT, w, k, KP, jacobi_max_sweeps(), sweeps);
   } else {
-    jacobi_kernel<false><<<1, JAC_THREADS, 0, s>>>(M, WT, w, k, KP, sweeps);
+    jacobi_kernel<false><<<1, JAC_THREADS, 0, s>>>(M, WT, w, k, KP, jacobi_max_sweeps(), sweeps);
   }
   eig_finish_kernel<<<std::max(1, std::min(64, g)), 256, 0, s>>>(w, WT, k, KP, P32, lam32, ub, wmm);
   dgemm_kp_kernel<false, true><<<g, 256, 0, s>>>(Bs, WT, Bt_out, KP);  // B_t = B_s P = B_s (Vᵀ)ᵀ

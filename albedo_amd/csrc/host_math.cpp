@@ -1,9 +1,11 @@
 // Host-side numerics of the engine: the fp64 symmetric eigensolver used to diagonalise the Gram
 // matrix each half-sweep, and the Spark-style (best effort) factor initialisation.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -327,12 +329,29 @@ void spark_initialize(const int32_t* ids_sorted, int64_t n, int rank, int64_t si
       for (int c = 0; c < rank; ++c) out[r * ld + c] = v[c] * inv;
     }
   };
+  if (n < (int64_t)1 << 16) {  // small inputs: no thread start-up
+    for (int b = 0; b < num_blocks; ++b) block(b);
+    return;
+  }
+  // a fixed pool of min(hardware threads, blocks) workers taking block indices from a counter (each
+  // block keeps its own generator, so the output does not depend on which worker draws it); a pool
+  // that cannot start a thread runs the remaining blocks on the caller's
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const int nw = (int)std::min<int64_t>(hw, num_blocks);
+  std::atomic<int> next{0};
+  auto worker = [&]() {
+    for (int b = next.fetch_add(1); b < num_blocks; b = next.fetch_add(1)) block(b);
+  };
   std::vector<std::thread> th;
-  for (int b = 0; b < num_blocks; ++b)
-    if (!rows[b].empty()) {
-      if (n < (int64_t)1 << 16) block(b);  // small inputs: no thread start-up
-      else th.emplace_back(block, b);
+  th.reserve(nw);
+  for (int w = 1; w < nw; ++w) {
+    try {
+      th.emplace_back(worker);
+    } catch (const std::system_error&) {
+      break;
     }
+  }
+  worker();
   for (auto& t : th) t.join();
 }
 

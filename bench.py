@@ -430,68 +430,72 @@ def cpu_baseline(lib, L, h, k, nnz, n_users, n_items, budget_s):
 
 
 def cpu_baseline_nnls(lib, L, h, k, nnz, n_users, n_items, budget_s):
-    """NNLS configs: the numpy fp64 restatement of Spark's NNLSSolver (oracle/spark_als.py nnls_solve,
-    one core: a row's projected-gradient loop is sequential) on a degree-stratified row sample; the
-    Gram of each src side by the C/OpenMP restatement.  A row's cost is its iteration count times a
-    k x k product, not its star count, so each stratum is extrapolated by its row count."""
-    from threadpoolctl import threadpool_limits
+    """NNLS configs: the fp64 C/OpenMP restatement of Spark's NNLSSolver (oracle/c/als_cpu.c
+    oracle_solve_rows_nnls: the normal equation as Spark builds it, fillAtA, NNLS.scala's projected
+    gradient with CG acceleration; equal to oracle/spark_als.py:nnls on the F5 rows, tests/test_oracle.py)
+    on every core this process may use, over a degree-stratified row sample.  A row's cost is its
+    iteration count times a k x k product, not its star count, so each stratum is extrapolated by its
+    row count.  The Gram of each src side by the C/OpenMP restatement."""
     from oracle import cbind
-    from oracle import spark_als as O
     info = host_cpu_info()
+    threads = info["usable"]
     res, t_sweep = {}, 0.0
-    with threadpool_limits(limits=1):
-        for dst, n_dst, n_src in ((0, n_users, n_items), (1, n_items, n_users)):
-            src = 1 - dst
-            sids = np.empty(n_src, np.int32)
-            sf = np.empty((n_src, k), np.float32)
-            L.check(lib.als_get_factors(h, src, L.ptr(sids, C.c_int32), L.ptr(sf, C.c_float)))
-            t0 = time.perf_counter()
-            G = cbind.gram(sf, threads=info["usable"])
-            g_s = time.perf_counter() - t0
-            dids = np.empty(n_dst, np.int32)
-            L.check(lib.als_get_ids(h, dst, L.ptr(dids, C.c_int32)))
-            deg = np.empty(n_dst, np.int64)
-            L.check(lib.als_get_degrees(h, dst, L.ptr(deg, C.c_int64)))
-            rng = np.random.default_rng(11 + dst)
-            edges = list(STRATA) + [int(deg.max()) + 1]
-            n_b = sum(1 for a, b in zip(edges[:-1], edges[1:]) if np.any((deg >= a) & (deg < b)))
-            strata, t_side = [], g_s
-            n_row = np.empty(1, np.int64)
-            for a, b in zip(edges[:-1], edges[1:]):
-                rows = np.nonzero((deg >= a) & (deg < b))[0]
-                if rows.size == 0:
-                    continue
-                order = rng.permutation(rows)
-                done, t_rows = 0, 0.0
-                while done < order.size and (t_rows < budget_s / (2 * n_b) or done == 0) and done < 4096:
-                    r = order[done]
-                    done += 1
+    for dst, n_dst, n_src in ((0, n_users, n_items), (1, n_items, n_users)):
+        src = 1 - dst
+        sids = np.empty(n_src, np.int32)
+        sf = np.empty((n_src, k), np.float32)
+        L.check(lib.als_get_factors(h, src, L.ptr(sids, C.c_int32), L.ptr(sf, C.c_float)))
+        t0 = time.perf_counter()
+        G = cbind.gram(sf, threads=threads)
+        g_s = time.perf_counter() - t0
+        dids = np.empty(n_dst, np.int32)
+        L.check(lib.als_get_ids(h, dst, L.ptr(dids, C.c_int32)))
+        deg = np.empty(n_dst, np.int64)
+        L.check(lib.als_get_degrees(h, dst, L.ptr(deg, C.c_int64)))
+        rng = np.random.default_rng(11 + dst)
+        edges = list(STRATA) + [int(deg.max()) + 1]
+        n_b = sum(1 for a, b in zip(edges[:-1], edges[1:]) if np.any((deg >= a) & (deg < b)))
+        strata, t_side = [], g_s
+        n_row = np.empty(1, np.int64)
+        for a, b in zip(edges[:-1], edges[1:]):
+            rows = np.nonzero((deg >= a) & (deg < b))[0]
+            if rows.size == 0:
+                continue
+            order = rng.permutation(rows)
+            done, t_rows, iters = 0, 0.0, 0
+            chunk = max(threads, 16)
+            while done < order.size and (t_rows < budget_s / (2 * n_b) or done == 0):
+                sel = order[done:done + chunk]
+                done += sel.size
+                ptr, cols, vals = [0], [], []
+                for r in sel:
                     m = int(deg[r])
                     bi, bv = np.empty(max(m, 1), np.int32), np.empty(max(m, 1), np.float32)
                     L.check(lib.als_get_row_ratings(h, dst, int(dids[r]), m, L.ptr(bi, C.c_int32),
                                                     L.ptr(bv, C.c_float), L.ptr(n_row, C.c_int64)))
-                    Y = sf[np.searchsorted(sids, bi[:m])].astype(np.float64)
-                    rv = bv[:m].astype(np.float64)
-                    t1 = time.perf_counter()
-                    c = 40.0 * np.abs(rv)
-                    A = G + (Y.T * c) @ Y
-                    bvec = Y.T @ np.where(rv > 0, 1.0 + c, 0.0)
-                    O.nnls_solve(A, bvec, 0.5 * float(np.sum(rv > 0)))
-                    t_rows += time.perf_counter() - t1
-                est = t_rows * rows.size / done
-                strata.append(dict(lo=a, rows=int(rows.size), sampled_rows=int(done), s=est))
-                t_side += est
-            res[dst] = dict(gram_s=g_s, strata=strata, side_s=t_side)
-            t_sweep += t_side
-            del sf
+                    cols.append(np.searchsorted(sids, bi[:m]).astype(np.int32))
+                    vals.append(bv[:m])
+                    ptr.append(ptr[-1] + m)
+                t1 = time.perf_counter()
+                _, it = cbind.solve_rows_nnls(sf, G, np.asarray(ptr, np.int64), np.concatenate(cols),
+                                              np.concatenate(vals), reg=0.5, alpha=40.0, threads=threads)
+                t_rows += time.perf_counter() - t1
+                iters += int(it.sum())
+                chunk = min(chunk * 2, 4096)
+            est = t_rows * rows.size / done
+            strata.append(dict(lo=a, rows=int(rows.size), sampled_rows=int(done), mean_iters=iters / done, s=est))
+            t_side += est
+        res[dst] = dict(gram_s=g_s, strata=strata, side_s=t_side)
+        t_sweep += t_side
+        del sf
     sampled = sum(st["sampled_rows"] for d in res for st in res[d]["strata"])
-    return {"value": nnz / t_sweep, "unit": "interactions/s", "cores": 1, "kind": "port",
+    return {"value": nnz / t_sweep, "unit": "interactions/s", "cores": threads, "kind": "port",
             "host": {k2: info[k2] for k2 in ("nproc", "affinity", "cgroup_quota", "model")},
             "sweep_s_extrapolated": t_sweep,
             "strata": {("user" if d == 0 else "item"): res[d]["strata"] for d in res},
-            "sample": (f"numpy fp64 restatement of Spark's NNLSSolver (oracle/spark_als.py nnls_solve, one core) on "
-                       f"{sampled} degree-stratified rows (strata {list(STRATA)}), each stratum extrapolated by its "
-                       f"row count; the Gram by the C/OpenMP restatement ({info['usable']} threads)")}
+            "sample": (f"fp64 C/OpenMP restatement of Spark's NNLSSolver (oracle/c/als_cpu.c oracle_solve_rows_nnls, "
+                       f"{threads} threads) on {sampled} degree-stratified rows (strata {list(STRATA)}), each stratum "
+                       f"extrapolated by its row count; the Gram by the C/OpenMP restatement")}
 
 
 if __name__ == "__main__":

@@ -174,9 +174,12 @@ int als_last_timings(const als_ctx* ctx, int dst_side, double* out, int n);
  * true "light" is the lockstep NNLS kernel (16 low-degree rows per workgroup) and "heavy" every
  * other row (one workgroup per row). */
 int als_path_stats(const als_ctx* ctx, int dst_side, int64_t* out4);
-/* NNLS iteration counts of the last half-sweep of dst_side (nonnegative = true):
- * out[0] = iterations summed over rows, out[1] = max over rows, out[2] = rows, out[3] = the part of
- * out[0] spent by the lockstep kernel's rows (als_path_stats out[0]). */
+/* Solver counters of the last half-sweep of dst_side.
+ * nonnegative = true (NNLS): out[0] = iterations summed over rows, out[1] = max over rows,
+ *   out[2] = rows, out[3] = the part of out[0] spent by the lockstep kernel's rows (als_path_stats out[0]).
+ * nonnegative = false (Cholesky path): out[0] = Jacobi sweeps the device eigensolver took on the src
+ *   Gram (0 without implicitPrefs), out[1..3] = 0.  A half-sweep whose eigensolver spends its sweep
+ *   budget without converging fails with ALS_E_NOT_POSITIVE_DEFINITE. */
 int als_solver_stats(const als_ctx* ctx, int dst_side, int64_t* out4);
 /* Top-k counters since als_create (als_recommend with k <= 64): out[0] = src rows through the MFMA
  * scan, out[1] = rows whose candidate set failed certification and were re-scored by the exact scan,

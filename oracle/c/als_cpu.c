@@ -7,6 +7,9 @@
  *                        b += (r > 0 ? 1 + c1 : 0) y (daxpy), n += (r > 0)
  *                        explicit: A += y yᵀ, b += r y, n += 1
  *   CholeskySolver       A += λ n I ; dppsv (Cholesky A = Uᵀ U + two triangular solves) ; to float
+ *   NNLSSolver           (nonnegative = true) fillAtA (full symmetric, A += λ n I) ; NNLS.solve
+ *                        (mllib/optimization/NNLS.scala: projected gradient with CG acceleration,
+ *                        restated in oracle/spark_als.py:nnls) ; to float
  * Used (a) by tests to cross-check the numpy restatement and (b) by bench.py as the timed
  * `cpu_baseline` ("port": Spark-algorithm CPU restatement, not Spark).
  */
@@ -138,6 +141,132 @@ int oracle_solve_rows(int64_t n_dst, const int64_t* ptr, const int32_t* col, con
   }
   free(Gp);
   return bad;
+}
+
+/* mllib/optimization/NNLS.scala solve (Spark 2.2.0), the numpy restatement oracle/spark_als.py:nnls
+ * (:247-299) line for line: ata full n x n (column-major = row-major, symmetric), ws = 5n doubles.
+ * Returns the iterations taken. */
+static int nnls_solve(int n, const double* ata, const double* atb, double* x, double* ws) {
+  double *grad = ws, *dir = ws + n, *last_dir = ws + 2 * n, *res = ws + 3 * n, *scratch = ws + 4 * n;
+  const int iter_max = n * 20 > 400 ? n * 20 : 400;
+  double last_norm = 0.0;
+  int iterno = 0, last_wall = 0;
+  for (int i = 0; i < n; ++i) x[i] = last_dir[i] = 0.0;
+#define NNLS_DOT(a, b) ({ double s_ = 0.0; for (int i_ = 0; i_ < n; ++i_) s_ += (a)[i_] * (b)[i_]; s_; })
+#define NNLS_GEMV(v, out) for (int r_ = 0; r_ < n; ++r_) { double s_ = 0.0; \
+    for (int c_ = 0; c_ < n; ++c_) s_ += ata[(int64_t)r_ * n + c_] * (v)[c_]; (out)[r_] = s_; }
+  while (iterno < iter_max) {
+    NNLS_GEMV(x, res);
+    for (int i = 0; i < n; ++i) {
+      res[i] -= atb[i];
+      grad[i] = (res[i] > 0.0 && x[i] == 0.0) ? 0.0 : res[i];
+    }
+    const double ngrad = NNLS_DOT(grad, grad);
+    for (int i = 0; i < n; ++i) dir[i] = grad[i];
+    NNLS_GEMV(grad, scratch);
+    double step = NNLS_DOT(grad, res) / (NNLS_DOT(scratch, grad) + 1e-20);
+    double ndir;
+    const double nx = NNLS_DOT(x, x);
+#define NNLS_STOP(st, nd) (isnan(st) || (st) < 1e-7 || (st) > 1e40 || (nd) < 1e-12 * nx || (nd) < 1e-32)
+    if (iterno > last_wall + 1) {
+      const double alpha = ngrad / last_norm;
+      for (int i = 0; i < n; ++i) dir[i] += alpha * last_dir[i];
+      NNLS_GEMV(dir, scratch);
+      const double dstep = NNLS_DOT(dir, res) / (NNLS_DOT(scratch, dir) + 1e-20);
+      ndir = NNLS_DOT(dir, dir);
+      if (NNLS_STOP(dstep, ndir)) {
+        for (int i = 0; i < n; ++i) dir[i] = grad[i];
+        ndir = NNLS_DOT(dir, dir);
+      } else {
+        step = dstep;
+      }
+    } else {
+      ndir = NNLS_DOT(dir, dir);
+    }
+    if (NNLS_STOP(step, ndir)) break;
+    for (int i = 0; i < n; ++i)
+      if (step * dir[i] > x[i]) step = x[i] / dir[i];
+    for (int i = 0; i < n; ++i) {
+      if (step * dir[i] > x[i] * (1 - 1e-14)) {
+        x[i] = 0.0;
+        last_wall = iterno;
+      } else {
+        x[i] -= step * dir[i];
+      }
+    }
+    ++iterno;
+    for (int i = 0; i < n; ++i) last_dir[i] = dir[i];
+    last_norm = ngrad;
+  }
+#undef NNLS_DOT
+#undef NNLS_GEMV
+#undef NNLS_STOP
+  return iterno;
+}
+
+/* oracle_solve_rows with Spark's NNLSSolver in place of the CholeskySolver (ALS with
+ * setNonnegative(true), ALSRecommenderBuilder.scala:46-56 surface): the same normal equation, then
+ * fillAtA + NNLS.solve per row, OpenMP over rows.  iters_out (may be NULL): per solved row (indexed
+ * like X_out) the NNLS iterations.  Returns 0. */
+int oracle_solve_rows_nnls(int64_t n_dst, const int64_t* ptr, const int32_t* col, const float* val,
+                           const float* Y, int k, int implicit, double alpha, double reg, const double* G,
+                           const int32_t* rows, int64_t n_rows, float* X_out, int32_t* iters_out, int nthreads) {
+  const int64_t tk = (int64_t)k * (k + 1) / 2;
+  if (!rows) n_rows = n_dst;
+#pragma omp parallel num_threads(nthreads)
+  {
+    double* ap = malloc(sizeof(double) * tk);
+    double* A = malloc(sizeof(double) * k * k);
+    double* b = malloc(sizeof(double) * k);
+    double* y = malloc(sizeof(double) * k);
+    double* x = malloc(sizeof(double) * k);
+    double* ws = malloc(sizeof(double) * 5 * k);
+#pragma omp for schedule(dynamic, 16)
+    for (int64_t q = 0; q < n_rows; ++q) {
+      const int64_t j = rows ? rows[q] : q;
+      if (implicit) {
+        for (int jj = 0; jj < k; ++jj)
+          for (int i = 0; i <= jj; ++i) ap[UP(i, jj)] = G[i * k + jj];
+      } else {
+        memset(ap, 0, sizeof(double) * tk);
+      }
+      memset(b, 0, sizeof(double) * k);
+      int64_t n = 0;
+      for (int64_t p = ptr[j]; p < ptr[j + 1]; ++p) {
+        const float* yr = Y + (int64_t)col[p] * k;
+        for (int c = 0; c < k; ++c) y[c] = yr[c];
+        const double r = val[p];
+        double cw, bw;
+        if (implicit) {
+          cw = alpha * fabs(r);
+          bw = r > 0.0 ? 1.0 + cw : 0.0;
+          if (r > 0.0) ++n;
+        } else {
+          cw = 1.0;
+          bw = r;
+          ++n;
+        }
+        if (cw != 0.0) dspr_upper(k, cw, y, ap);
+        if (bw != 0.0)
+          for (int c = 0; c < k; ++c) b[c] += bw * y[c];
+      }
+      /* NNLSSolver.fillAtA: the full symmetric matrix, λ n on the diagonal */
+      const double lam = reg * (double)n;
+      for (int jj = 0; jj < k; ++jj)
+        for (int i = 0; i <= jj; ++i) A[(int64_t)i * k + jj] = A[(int64_t)jj * k + i] = ap[UP(i, jj)];
+      for (int c = 0; c < k; ++c) A[(int64_t)c * k + c] += lam;
+      const int it = nnls_solve(k, A, b, x, ws);
+      if (iters_out) iters_out[j] = it;
+      for (int c = 0; c < k; ++c) X_out[j * k + c] = (float)x[c];
+    }
+    free(ap);
+    free(A);
+    free(b);
+    free(y);
+    free(x);
+    free(ws);
+  }
+  return 0;
 }
 
 int oracle_half_sweep(int64_t n_dst, const int64_t* ptr, const int32_t* col, const float* val,

@@ -21,6 +21,9 @@ def load():
         _lib.oracle_solve_rows.restype = C.c_int
         _lib.oracle_solve_rows.argtypes = [C.c_int64, P, P, P, P, C.c_int, C.c_int, C.c_double, C.c_double, P, P,
                                            C.c_int64, P, C.c_int]
+        _lib.oracle_solve_rows_nnls.restype = C.c_int
+        _lib.oracle_solve_rows_nnls.argtypes = [C.c_int64, P, P, P, P, C.c_int, C.c_int, C.c_double, C.c_double, P,
+                                                P, C.c_int64, P, P, C.c_int]
         _lib.oracle_gram.restype = C.c_int
         _lib.oracle_gram.argtypes = [C.c_int64, C.c_int, P, P, C.c_int]
         _lib.oracle_max_threads.restype = C.c_int
@@ -76,6 +79,23 @@ def solve_rows(Ysrc, G, ptr, col, val, *, reg, alpha, implicit=True, threads=Non
     if rc != 0:
         raise ValueError(f"oracle solve_rows: row {rc - 1} not positive definite (rc={rc})")
     return X
+
+
+def solve_rows_nnls(Ysrc, G, ptr, col, val, *, reg, alpha, implicit=True, threads=None):
+    """solve_rows with Spark's NNLSSolver (setNonnegative(true)): (X [n_dst, k], NNLS iterations per row)."""
+    lib = load()
+    Ysrc = np.ascontiguousarray(Ysrc, dtype=np.float32)
+    G = np.ascontiguousarray(G, dtype=np.float64)
+    ptr = np.ascontiguousarray(ptr, dtype=np.int64)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    val = np.ascontiguousarray(val, dtype=np.float32)
+    n_dst = len(ptr) - 1
+    k = Ysrc.shape[1]
+    X = np.zeros((n_dst, k), dtype=np.float32)
+    it = np.zeros(n_dst, dtype=np.int32)
+    lib.oracle_solve_rows_nnls(n_dst, _p(ptr), _p(col), _p(val), _p(Ysrc), k, int(implicit), float(alpha),
+                               float(reg), _p(G), None, 0, _p(X), _p(it), threads or lib.oracle_max_threads())
+    return X, it
 
 
 def recommend(src_f, dst_ids, dst_f, num, threads=None):

@@ -839,3 +839,35 @@ def test_device_eigensolver(gpu_lib, k):
         assert np.abs(np.sort(w) - np.linalg.eigvalsh(g)).max() < 1e-12 * gn, name
     assert np.abs(np.sort(out["cold"][0]) - ref).max() < 1e-12 * np.linalg.norm(G)
     assert out["cold"][2] <= 12 and out["warm"][2] <= out["cold"][2], (out["cold"][2], out["warm"][2])
+
+
+@pytest.mark.parametrize("k", [50, 200])
+def test_eigensolver_budget_exhausted_raises(gpu_lib, monkeypatch, k):
+    """A Jacobi run that spends its sweep budget without converging is an error, as the host
+    eigensolver's "did not converge" was: als_device_eigh and a half-sweep both fail with
+    ALS_E_NOT_POSITIVE_DEFINITE instead of solving in a basis that does not diagonalise the Gram.
+    ALBEDO_JAC_MAX_SWEEPS=1 (test knob) forces it; the default budget then solves the same inputs."""
+    from albedo_amd import _lib as L
+    from albedo_amd.synthetic import SynthSpec, generate
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((4000, k)) * np.logspace(0, 2, k)
+    G = np.ascontiguousarray(X.T @ X)
+    w = np.empty(k)
+    V = np.empty((k, k))
+    sw = np.zeros(1, np.int32)
+    args = (0, k, L.ptr(G, C.c_double), None, L.ptr(w, C.c_double), L.ptr(V, C.c_double), L.ptr(sw, C.c_int32))
+    monkeypatch.setenv("ALBEDO_JAC_MAX_SWEEPS", "1")
+    assert gpu_lib.als_device_eigh(*args) == 2
+    assert "did not converge" in gpu_lib.als_last_error().decode()
+    d = generate(SynthSpec(800, 300, 12000, seed=k))
+    B = O.make_blocks(d["user"], d["item"], d["rating"])
+    c = Ctx(gpu_lib, k)
+    c.ratings(d["user"], d["item"], d["rating"])
+    c.inject(0, B.user_ids, rng.standard_normal((len(B.user_ids), k)).astype(np.float32))
+    c.inject(1, B.item_ids, np.zeros((len(B.item_ids), k), np.float32))
+    assert gpu_lib.als_half_sweep(c.h, 1) == 2
+    assert "did not converge" in gpu_lib.als_last_error().decode()
+    monkeypatch.delenv("ALBEDO_JAC_MAX_SWEEPS")
+    L.check(gpu_lib.als_device_eigh(*args))
+    assert 1 < sw[0] <= 12
+    c.half(1)

@@ -158,3 +158,19 @@ def test_c_topk_oracle_matches_numpy_oracle_and_golden():
     a = O.recommend_for_all(np.arange(5), uf[:5], iid[:20], itf[:20], 30)
     b = cbind.recommend(uf[:5], iid[:20], itf[:20], 30)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1][:, :20], b[1][:, :20]) and np.all(np.isnan(b[1][:, 20:]))
+
+
+def test_c_nnls_matches_numpy_nnls_on_f5():
+    """The C/OpenMP NNLSSolver restatement (oracle/c/als_cpu.c, the c5 bench's cpu_baseline) equals the
+    numpy restatement of NNLS.scala (oracle/spark_als.py:nnls) on the F5 golden rows: the committed
+    item half-sweep V1 from U0, and the user half-sweep from V1, row by row."""
+    f = _load("f5_nnls.npz")
+    B = O.make_blocks(f["user"], f["item"], f["rating"])
+    U0 = f["U0"].astype(np.float32)
+    V, it = cbind.solve_rows_nnls(U0, O.gram(U0), B.i_ptr, B.i_col, B.i_val, reg=0.5, alpha=40.0, threads=4)
+    assert np.all(V >= 0) and np.all(it > 0)
+    assert np.allclose(V, f["V1"], rtol=1e-6, atol=1e-7)
+    U, _ = cbind.solve_rows_nnls(V, O.gram(V), B.u_ptr, B.u_col, B.u_val, reg=0.5, alpha=40.0, threads=3)
+    U_ref = O.half_sweep(V, B.u_ptr, B.u_col, B.u_val, reg=0.5, alpha=40.0, nonnegative=True)
+    assert np.allclose(U, U_ref, rtol=1e-6, atol=1e-7)
+    assert np.mean((U == 0) == (U_ref == 0)) == 1.0
