@@ -90,7 +90,7 @@ struct DevBuf {
   T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-enum { B_L16 = 0, B_L32 = 1, B_L64 = 2, B_HEAVY = 3, NBUCKET = 4 };
+enum { B_L16 = 0, B_L32 = 1, B_L64 = 2, B_L96 = 3, B_HEAVY = 4, NBUCKET = 5 };
 
 struct Side {
   int64_t n = 0;                 // rows (unique raw ids)
@@ -222,8 +222,11 @@ int validate(const als_params* p) {
   return ALS_OK;
 }
 
+// Rows of degree <= light_limit take the push-through solve (a d x d system).  d <= 64 by default;
+// light_max_degree up to 96 (KP = 128) routes rows of degree 65..96 through the d x d path too
+// (solve_light_kernel<128, 96>), measured against the explicit k x k wave kernel in DESIGN §4.
 int64_t light_limit(const als_ctx* c) {
-  if (c->p.light_max_degree >= 0) return std::min<int64_t>(c->p.light_max_degree, 64);
+  if (c->p.light_max_degree >= 0) return std::min<int64_t>(c->p.light_max_degree, c->KP == 128 ? 96 : 64);
   return c->KP >= 128 ? 64 : 32;
 }
 
@@ -231,7 +234,7 @@ int bucket_of(int64_t d, int64_t lmax) {
   if (d <= lmax) {
     if (d <= 16) return B_L16;
     if (d <= 32) return B_L32;
-    return B_L64;
+    return d <= 64 ? B_L64 : B_L96;
   }
   return B_HEAVY;
 }
@@ -931,9 +934,9 @@ int half_sweep(als_ctx* c, int t) {
   a.colscale = c->d_cs.as<float>();
   a.n_cu = c->n_cu;
   const int32_t* rows = T.d_rows.as<int32_t>();
-  static const int Dof[3] = {16, 32, 64};
+  static const int Dof[B_HEAVY] = {16, 32, 64, 96};
   T.stats[0] = T.stats[1] = T.stats[2] = T.stats[3] = 0;
-  for (int b = 0; b < 3; ++b) {
+  for (int b = 0; b < B_HEAVY; ++b) {
     T.stats[force_heavy ? 2 : 0] += T.boff[b + 1] - T.boff[b];
     T.stats[force_heavy ? 3 : 1] += T.bnnz[b];
   }
@@ -942,7 +945,7 @@ int half_sweep(als_ctx* c, int t) {
   // Solve chunk by chunk (one chunk unless world > 1); world > 1: each finished chunk of the new
   // factors is gathered on the second stream while the next chunk solves
   for (int q = 0; q < T.nsolve; ++q) {
-    for (int b = 0; b < 3; ++b) {
+    for (int b = 0; b < B_HEAVY; ++b) {
       a.rows = rows + T.cb[b][q];
       a.desc = T.d_desc.as<int32_t>() + 4 * T.cb[b][q];
       a.n_rows = T.cb[b][q + 1] - T.cb[b][q];

@@ -659,26 +659,34 @@ __host__ __device__ constexpr int light_wave_lds(int D) { return D == 16 ? D * (
 // workgroups per CU: D = 32 at KP = 128 keeps its gathered rows in registers (KEEPZ) and spilled 16
 // VGPRs at 4 (128 VGPRs); at 3 (168) it does not, and the user light half is 1.9 ms faster (r04 A/B)
 template <int KP, int D>
-constexpr int light_occupancy() { return (D == 16 && KP <= 128) ? 6 : (KP == 128 && D == 32) ? 3 : (KP <= 128) ? 4 : 2; }
+constexpr int light_occupancy() {
+  return D > 64 ? 2 : (D == 16 && KP <= 128) ? 6 : (KP == 128 && D == 32) ? 3 : (KP <= 128) ? 4 : 2;
+}
 
-// One light row: j, degree d (wave-uniform), lane e < d holds rating r and src row colE of entry e.
+// One light row: j, degree d (wave-uniform), lane e < d holds rating r and src row colE of entry e;
+// D > 64: lane e also holds entry 64 + e (r2, colE2).
 template <int KP, int D>
-__device__ __forceinline__ void light_row(const SolveArgs& a, int j, int d, float r, int colE, float* smem, int wave) {
+__device__ __forceinline__ void light_row(const SolveArgs& a, int j, int d, float r, int colE, float r2, int colE2,
+                                          float* smem, int wave) {
   constexpr int NB = D / 16, NT = NB * (NB + 1) / 2, TRI = light_wave_lds(D), NHC = KP / 64;
+  constexpr bool TWO = D > 64;  // two entries per lane
   const int lane = threadIdx.x & 63, g = lane >> 4, i16 = lane & 15;
   float* Ks = smem + wave * TRI;
-  float ce = 0.f, we = 0.f;
+  float ce = 0.f, we = 0.f, ce2 = 0.f, we2 = 0.f;
   if (lane < d) rating_weights(r, a.implicit, a.alpha, ce, we);
+  if (TWO && 64 + lane < d) rating_weights(r2, a.implicit, a.alpha, ce2, we2);
   const bool valid = lane < d && ce > 0.f;
-  const int npos = a.implicit ? __popcll(__ballot(lane < d && r > 0.f)) : d;
+  const bool valid2 = TWO && 64 + lane < d && ce2 > 0.f;
+  const int npos = a.implicit ? __popcll(__ballot(lane < d && r > 0.f)) + (TWO ? __popcll(__ballot(64 + lane < d && r2 > 0.f)) : 0)
+                              : d;
   const float lamn = a.reg * (float)npos;
 
   int colB[NB];
   bool vB[NB];
 #pragma unroll
   for (int I = 0; I < NB; ++I) {
-    colB[I] = __shfl(colE, 16 * I + i16);
-    vB[I] = __shfl((int)valid, 16 * I + i16) != 0;
+    colB[I] = __shfl(I < 4 ? colE : colE2, 16 * (I & 3) + i16);
+    vB[I] = __shfl((int)(I < 4 ? valid : valid2), 16 * (I & 3) + i16) != 0;
   }
   constexpr int NC = KP / 16;
   constexpr bool KEEPZ = D <= 32 && D * KP <= 4096;  // keep the gathered rows in registers for x' (D = 64 at KP = 128, 2 waves per SIMD: measured slower)
@@ -703,7 +711,7 @@ __device__ __forceinline__ void light_row(const SolveArgs& a, int j, int d, floa
     sdl[cc] = (cc < a.kreal && dd > 0.f) ? frsq(dd) : 0.f;
   }
   WAVE_LDS_SYNC();
-  if constexpr (D == 64 || KEEPZ) {
+  if constexpr (D >= 64 || KEEPZ) {
     // S on split-fp16 MFMA (hi·hi + hi·lo + lo·hi, 32 columns per instruction: at D = 64 120 instead
     // of 320 fp32 MFMAs, at D = 16 12 x 16 cycles instead of 32 x 32).  One power-of-two scale for the
     // whole row (so S unscales exactly): |Z[.][c]| < 2^(13 - e_c) (colscale), hence
@@ -779,7 +787,8 @@ __device__ __forceinline__ void light_row(const SolveArgs& a, int j, int d, floa
   }
   if (__any(bad) && lane == 0) atomicOr(a.err, 1);
   const float cinv = valid ? frcp(ce) : 0.f;
-  float y;  // lane e < d: v_e on return
+  const float cinv2 = valid2 ? frcp(ce2) : 0.f;
+  float y, y2 = 0.f;  // lane e < d: v_e on return (y2: v_{64+e})
   if constexpr (D == 16) {  // register Cholesky, lane i = row i, DPP broadcasts
     // S -> LDS (only the lower triangle is read by the Cholesky below)
     static_for<0, NT>([&](auto t) {
@@ -846,21 +855,25 @@ __device__ __forceinline__ void light_row(const SolveArgs& a, int j, int d, floa
     // K = S + C⁻¹ (identity rows for masked entries), factored in the accumulators (wave_chol.h):
     // the diagonal of tile (A, A) sits in lane i + 16q, slot r with 4q + r == i
     const float dadd = valid ? cinv : 1.0f, rhs = valid ? we * cinv : 0.f;
+    const float dadd2 = valid2 ? cinv2 : 1.0f, rhs2 = valid2 ? we2 * cinv2 : 0.f;
     float bacc[NB];
     static_for<0, NB>([&](auto AA) {
       constexpr int A = decltype(AA)::value, t = tix(A, A, NB);
-      const float dA = __shfl(dadd, 16 * A + i16);
+      const float dA = __shfl(A < 4 ? dadd : dadd2, 16 * (A & 3) + i16);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (4 * g + r == i16) acc[t][r] += dA;
-      bacc[A] = __shfl(rhs, 16 * A + i16);
+      bacc[A] = __shfl(A < 4 ? rhs : rhs2, 16 * (A & 3) + i16);
     });
     float xs[NB];
-    const bool notpd = wave_chol_solve<NB>(acc, bacc, Ks, xs);
+    const bool notpd = WAVE_CHOL_SOLVE<NB>(acc, bacc, Ks, xs);
     if (notpd && lane == 0) atomicOr(a.err, 2 | ALBEDO_EF_LIGHT_ACC);
-    y = 0.f;  // lane 16A + i holds v[16A + i] = xs[A] (its own slot A = g)
+    y = 0.f;  // lane 16A + i holds v[16A + i] = xs[A] (its own slot A = g); y2: v[64 + 16A + i]
 #pragma unroll
-    for (int A = 0; A < NB; ++A) y = g == A ? xs[A] : y;
+    for (int A = 0; A < NB; ++A) {
+      if (A < 4) y = g == A ? xs[A] : y;
+      else y2 = g == A - 4 ? xs[A] : y2;
+    }
   }
   // x' = D⁻¹ Zᵀ v
   if constexpr (KEEPZ) {
@@ -890,9 +903,10 @@ __device__ __forceinline__ void light_row(const SolveArgs& a, int j, int d, floa
       float ve[8], zz[8][NHC];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int e = e0 + u < d ? e0 + u : d - 1;
-        ve[u] = e0 + u < d ? rdlane(y, e) : 0.f;
-        const float* zr = a.Z + (int64_t)rdlane_i(colE, e) * KP + lane;
+        const int e = e0 + u < d ? e0 + u : d - 1;  // wave-uniform
+        const bool hi = TWO && e >= 64;
+        ve[u] = e0 + u < d ? rdlane(hi ? y2 : y, e & 63) : 0.f;
+        const float* zr = a.Z + (int64_t)rdlane_i(hi ? colE2 : colE, e & 63) * KP + lane;
 #pragma unroll
         for (int h = 0; h < NHC; ++h) zz[u][h] = zr[64 * h];
       }
@@ -924,13 +938,17 @@ __global__ __launch_bounds__(256, (light_occupancy<KP, D>())) void solve_light_k
   cint* q = (cint*)(a.desc) + 4 * ridx;  // constant address space: s_load_dwordx4
   const int j = q[0], d = q[3];
   const int64_t p0 = (int64_t)(uint32_t)q[1] | ((int64_t)q[2] << 32);
-  float r = 0.f;
-  int colE = 0;
+  float r = 0.f, r2 = 0.f;
+  int colE = 0, colE2 = 0;
   if (lane < d) {
     r = a.val[p0 + lane];
     colE = a.col[p0 + lane];
   }
-  light_row<KP, D>(a, j, d, r, colE, smem, wave);
+  if (D > 64 && 64 + lane < d) {
+    r2 = a.val[p0 + 64 + lane];
+    colE2 = a.col[p0 + 64 + lane];
+  }
+  light_row<KP, D>(a, j, d, r, colE, r2, colE2, smem, wave);
 }
 
 hipError_t launch_solve_light(int KP, int D, const SolveArgs& a0, hipStream_t s) {
@@ -951,7 +969,7 @@ hipError_t launch_solve_light(int KP, int D, const SolveArgs& a0, hipStream_t s)
 #define LIGHT(kp, dd) \
   if (KP == kp && D == dd) { solve_light_kernel<kp, dd><<<blocks, 256, lds, s>>>(a); return hipGetLastError(); }
   LIGHT(64, 16) LIGHT(64, 32) LIGHT(64, 64) LIGHT(128, 16) LIGHT(128, 32) LIGHT(128, 64)
-  LIGHT(256, 16) LIGHT(256, 32) LIGHT(256, 64)
+  LIGHT(256, 16) LIGHT(256, 32) LIGHT(256, 64) LIGHT(128, 96)
 #undef LIGHT
   return hipErrorInvalidValue;
 }

@@ -173,6 +173,19 @@ __device__ __forceinline__ double tk_err(double ns, const TopkArgs& a) {
   return rel * ns * tm + absu;
 }
 
+#ifdef ALBEDO_TOPK_PHASES  // probe builds only (tools/topk_phases.py): shader-clock time per scan phase
+__device__ unsigned long long g_tk_ph[16];  // [0..7] cycles per phase summed over waves, [8..15] event counts
+#define TKPH_T0() unsigned long long tk_t = __builtin_amdgcn_s_memtime(), tk_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tk_n[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define TKPH(k) { const unsigned long long tk_x = __builtin_amdgcn_s_memtime(); tk_acc[k] += tk_x - tk_t; tk_t = tk_x; }
+#define TKPH_N(k, v) tk_n[k] += (v)
+#define TKPH_OUT() if ((threadIdx.x & 63) == 0) for (int k_ = 0; k_ < 8; ++k_) { atomicAdd(&g_tk_ph[k_], tk_acc[k_]); atomicAdd(&g_tk_ph[8 + k_], tk_n[k_]); }
+#else
+#define TKPH_T0()
+#define TKPH(k)
+#define TKPH_N(k, v)
+#define TKPH_OUT()
+#endif
+
 template <int KP, int G>
 __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
   using C = TkScan<KP, G>;
@@ -281,6 +294,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
     }
   }
 
+  TKPH_T0();
   // candidates of one 16-row tile (dst positions jt .. jt+15).  Slots come from a ballot prefix count
   // over the 16 lanes of a row's group; list lengths live in registers, one byte per row (cntp[gi]
   // byte r: row 16gi + 4g + r, the same in the 16 lanes of group g), so the append path touches no
@@ -292,6 +306,8 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[gi][r]);
     if (!__any(mx >= 0.f)) return;
+    TKPH(2);
+    TKPH_N(2, 1);
     const int64_t dj = jt + i16;
     const bool dv = dj < a.n_dst;
     const uint32_t below = (1u << i16) - 1u;
@@ -316,6 +332,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
           over |= ncnt > TRIG;
         }
       }
+    TKPH(3);  // appends
     if (!__any(over)) return;
     // wave-local rows to compact (bit 16gi + 4g + r)
     uint64_t f0 = 0, f1 = 0;
@@ -332,7 +349,10 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
           }
       }
     const uint64_t d0 = f0, d1 = f1;
+    TKPH_N(3, 1);
+    TKPH_N(4, __popcll(f0) + __popcll(f1));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's list stores are in L2
+    TKPH(6);  // the drain of every outstanding VMEM op (ring DMAs included) before a compaction
     while (f0 | f1) {
       int wl;
       if (f0) { wl = __builtin_ctzll(f0); f0 &= f0 - 1; }
@@ -370,10 +390,12 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
           cntp[gi] = (cntp[gi] & ~(0xffu << (8 * r))) | (64u << (8 * r));
         }
       }
+    TKPH(4);  // compaction loads + sorts + stores
   };
 
   int64_t it = 0, n_scored = 0;  // chunk iterations; chunks this wave scored (its `need` held)
   for (int64_t c = next_chunk(-1); c < nch; c = next_chunk(c), ++it) {
+    TKPH(5);  // next_chunk (mask walk)
     // this wave's DMAs of chunk c have landed (in-order VM counter; later list stores only make the
     // wait stricter), then one barrier publishes every wave's part and retires the previous slot
     if (n_iss - it - 1 >= C::NSTG - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NVM * (C::NSTG - 2)) : "memory");
@@ -387,6 +409,8 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
         ++n_iss;
       }
     }
+    TKPH(0);  // DMA wait + barrier + next DMA issue
+    TKPH_N(0, 1);
     // can any row of this wave still take a dst row of chunk c (bound + margin >= its threshold)?
     const char* base = ring + (int)(it % C::NSTG) * C::SLOT;
     bool need = !a.cfeat;
@@ -408,8 +432,10 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
         }
       }
     }
+    TKPH(1);  // chunk bound test
     if (!__any(need)) continue;
     ++n_scored;
+    TKPH_N(1, 1);
     const int64_t j0 = c * C::CH;
     f16x8 df[2][NQ];
     auto rd = [&](int J, f16x8 (&d)[NQ]) __attribute__((always_inline)) {
@@ -432,7 +458,9 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       if constexpr (J > 0) check_tile(acc[(J - 1) & 1], j0 + 16 * (J - 1));
     });
     check_tile(acc[(NJ - 1) & 1], j0 + 16 * (NJ - 1));
+    TKPH(2);  // MFMA scoring + tile checks (appends / compactions below are subtracted out)
   }
+  TKPH_OUT();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup ends
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (i16 == 0) {
@@ -1074,6 +1102,17 @@ hipError_t launch_topk(int KP, const TopkArgs& a, int n_cu, hipStream_t s) {
   if (KP == 256) return launch_topk_kp<256>(a, n_cu, s);
   return hipErrorInvalidValue;
 }
+
+#ifdef ALBEDO_TOPK_PHASES
+extern "C" int als_debug_topk_phases(unsigned long long* out16, int reset) {
+  if (out16 && hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_tk_ph), 16 * 8) != hipSuccess) return 4;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_tk_ph), z, sizeof z) != hipSuccess) return 4;
+  }
+  return 0;
+}
+#endif
 
 hipError_t launch_topk_select(int KP, const TopkArgs& a, hipStream_t s) {
   if (a.n_src <= 0) return hipSuccess;

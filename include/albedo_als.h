@@ -59,7 +59,8 @@ typedef struct als_params {
   double alpha;            /* setAlpha, default 1.0, >= 0 */
   int64_t seed;            /* setSeed, default = hash of the class name in Spark; here 0 if unset */
   int32_t device;          /* HIP device ordinal; -1 = current device */
-  int32_t light_max_degree;/* rows with <= this many ratings take the rotated push-through solve;
+  int32_t light_max_degree;/* rows with <= this many ratings take the rotated push-through solve (capped at
+                              96 at rank 65..128, 64 otherwise);
                               -1 = engine default, 0 = every row takes the explicit Cholesky solve */
 } als_params;
 

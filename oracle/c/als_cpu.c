@@ -204,6 +204,16 @@ static int nnls_solve(int n, const double* ata, const double* atb, double* x, do
   return iterno;
 }
 
+/* NNLS.solve on one dense system (ata full n x n with λ n already on its diagonal): x (n doubles) and the
+ * iterations taken */
+int oracle_nnls_dense(int n, const double* ata, const double* atb, double* x) {
+  double* ws = malloc(sizeof(double) * 5 * n);
+  if (!ws) return -1;
+  const int it = nnls_solve(n, ata, atb, x, ws);
+  free(ws);
+  return it;
+}
+
 /* oracle_solve_rows with Spark's NNLSSolver in place of the CholeskySolver (ALS with
  * setNonnegative(true), ALSRecommenderBuilder.scala:46-56 surface): the same normal equation, then
  * fillAtA + NNLS.solve per row, OpenMP over rows.  iters_out (may be NULL): per solved row (indexed

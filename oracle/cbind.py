@@ -24,6 +24,8 @@ def load():
         _lib.oracle_solve_rows_nnls.restype = C.c_int
         _lib.oracle_solve_rows_nnls.argtypes = [C.c_int64, P, P, P, P, C.c_int, C.c_int, C.c_double, C.c_double, P,
                                                 P, C.c_int64, P, P, C.c_int]
+        _lib.oracle_nnls_dense.restype = C.c_int
+        _lib.oracle_nnls_dense.argtypes = [C.c_int, P, P, P]
         _lib.oracle_gram.restype = C.c_int
         _lib.oracle_gram.argtypes = [C.c_int64, C.c_int, P, P, C.c_int]
         _lib.oracle_max_threads.restype = C.c_int
@@ -96,6 +98,19 @@ def solve_rows_nnls(Ysrc, G, ptr, col, val, *, reg, alpha, implicit=True, thread
     lib.oracle_solve_rows_nnls(n_dst, _p(ptr), _p(col), _p(val), _p(Ysrc), k, int(implicit), float(alpha),
                                float(reg), _p(G), None, 0, _p(X), _p(it), threads or lib.oracle_max_threads())
     return X, it
+
+
+def nnls_dense(A, b):
+    """NNLS.solve (fp64, oracle/c/als_cpu.c) on one system A x = b, A with λn on its diagonal:
+    (x as float32 -- NNLSSolver's cast --, iterations)."""
+    lib = load()
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros(len(b))
+    it = lib.oracle_nnls_dense(len(b), _p(A), _p(b), _p(x))
+    if it < 0:
+        raise MemoryError("oracle_nnls_dense")
+    return x.astype(np.float32), it
 
 
 def recommend(src_f, dst_ids, dst_f, num, threads=None):

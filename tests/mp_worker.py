@@ -20,6 +20,7 @@ def main():
     import torch
     import torch.distributed as dist
     mode, out = sys.argv[1], sys.argv[2]
+    k = int(sys.argv[3]) if len(sys.argv) > 3 else 16
     dist.init_process_group("gloo", init_method="env://")
     rank, world = dist.get_rank(), dist.get_world_size()
     from albedo_amd import _lib as L
@@ -28,7 +29,6 @@ def main():
     lib = L.load()
     d = generate(SynthSpec(1200, 400, 16000, seed=41))
     B = O.make_blocks(d["user"], d["item"], d["rating"])
-    k = 16
     rng = np.random.default_rng(3)
     U0 = rng.standard_normal((len(B.user_ids), k)).astype(np.float32)
     V0 = rng.standard_normal((len(B.item_ids), k)).astype(np.float32)

@@ -125,7 +125,7 @@ def test_golden_f1_half_sweep_and_gram(gpu_lib, k):
             assert st[0] == 0
 
 
-@pytest.mark.parametrize("k,light", [(50, -1), (50, 0), (64, -1), (100, -1), (128, 0), (128, -1), (200, -1),
+@pytest.mark.parametrize("k,light", [(50, -1), (50, 0), (64, -1), (100, -1), (128, 0), (128, -1), (128, 96), (200, -1),
                                      (256, 0), (256, -1)])
 def test_half_sweep_ranks_and_paths(gpu_lib, k, light):
     from albedo_amd.synthetic import SynthSpec, generate

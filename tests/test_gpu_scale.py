@@ -183,14 +183,27 @@ def test_c4_scale_rows_match_fp64_solve(gpu_lib, c4_ctx):
 
 @pytest.mark.timeout(900)
 def test_c4_topk_converged_factors(gpu_lib, c4_ctx):
-    """On factors after 20 sweeps (the driver's bench scores top-k after 25): 200 user rows of the
-    20th sweep equal the fp64 solve of Spark's normal equation built from the engine's own CSR and
-    item factors; then top-30 over all 20M users, 2,000 sampled users plus 2,000 of the exact-rescan
-    users (all of them when fewer) bit-exact against the oracle."""
+    """On factors after 20 sweeps (the driver's bench scores top-k after 25): the 20th sweep's item
+    half -- the three most starred repos (10^6+ stars, split-K), 20 rows of degree 65-128 (the rows
+    nearest the light limit on the wave kernel) and 30 random repos -- and 200 user rows of its user
+    half equal the fp64 solve of Spark's normal equation built from the engine's own CSR and src
+    factors; then top-30 over all 20M users, 2,000 sampled users plus 2,000 of the exact-rescan users
+    (all of them when fewer) bit-exact against the oracle."""
+    from albedo_amd import _lib as L
     c = c4_ctx
     _sweeps(c, 18)
+    uids, U19 = c.factors(0)
     c.half(1)
     iids, V = c.factors(1)
+    ideg = np.empty(iids.size, np.int64)
+    L.check(gpu_lib.als_get_degrees(c.h, 1, L.ptr(ideg, C.c_int64)))
+    rng = np.random.default_rng(19)
+    top = iids[np.argsort(-ideg, kind="stable")[:3]]
+    mid = rng.choice(iids[(ideg > 64) & (ideg <= 128)], 20, replace=False)
+    worst = _check_rows_fp64(gpu_lib, c, 1, np.r_[top, mid, rng.choice(iids, 30, replace=False)], iids, V, uids, U19,
+                             128)
+    print(f"c4 sweep-20 item rows: worst rel err {worst:.2e}")
+    del U19
     c.half(0)
     uids, U = c.factors(0)
     rng = np.random.default_rng(20)

@@ -19,13 +19,13 @@ def _free_port():
     return p
 
 
-def _launch(mode, out, world=2, timeout=300, env_extra=None):
+def _launch(mode, out, world=2, timeout=300, env_extra=None, k=16):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), **(env_extra or {}))
-        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_worker.py"), mode, out],
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_worker.py"), mode, out, str(k)],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     outs = []
     for p in procs:
@@ -41,14 +41,28 @@ def _launch(mode, out, world=2, timeout=300, env_extra=None):
     return np.load(out)
 
 
-def _problem():
+def _problem(k=16):
     from albedo_amd.synthetic import SynthSpec, generate
     d = generate(SynthSpec(1200, 400, 16000, seed=41))
     B = O.make_blocks(d["user"], d["item"], d["rating"])
     rng = np.random.default_rng(3)
-    U0 = rng.standard_normal((len(B.user_ids), 16)).astype(np.float32)
-    V0 = rng.standard_normal((len(B.item_ids), 16)).astype(np.float32)
+    U0 = rng.standard_normal((len(B.user_ids), k)).astype(np.float32)
+    V0 = rng.standard_normal((len(B.item_ids), k)).astype(np.float32)
     return B, U0, V0
+
+
+def _fit_ref(B, U0, V0, k, max_iter, nonneg):
+    """O.fit (Spark order: item half, then user half); the NNLS halves through the C restatement of
+    NNLSSolver (oracle/c/als_cpu.c, equal to oracle/spark_als.py:nnls: tests/test_oracle.py) so that
+    rank 256 stays within seconds."""
+    if not nonneg:
+        return O.fit(B, rank=k, max_iter=max_iter, reg=0.5, alpha=40.0, init_user=U0, init_item=V0)
+    from oracle import cbind
+    U, V = U0, V0
+    for _ in range(max_iter):
+        V, _ = cbind.solve_rows_nnls(U, O.gram(U), B.i_ptr, B.i_col, B.i_val, reg=0.5, alpha=40.0)
+        U, _ = cbind.solve_rows_nnls(V, O.gram(V), B.u_ptr, B.u_col, B.u_val, reg=0.5, alpha=40.0)
+    return U, V
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -62,24 +76,31 @@ def test_sharded_layout_cpu(tmp_path, world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,nonneg,split", [(2, False, 0), (3, False, 0), (3, True, 0), (2, False, 128),
-                                                (3, False, 128), (3, True, 128)])
-def test_sharded_fit_gpu_matches_single(gpu_lib, tmp_path, world, nonneg, split):
+@pytest.mark.parametrize("world,nonneg,split,k", [(2, False, 0, 16), (3, False, 0, 16), (3, True, 0, 16),
+                                                  (2, False, 128, 16), (3, False, 128, 16), (3, True, 128, 16),
+                                                  (2, False, 128, 128), (3, False, 128, 128), (3, True, 128, 256)])
+def test_sharded_fit_gpu_matches_single(gpu_lib, tmp_path, world, nonneg, split, k):
     """Ranks sharing the box's GPU run the engine's sharded fit (device remap into the chunk-major
     gathered layout, the solve in row chunks whose factors are gathered on a second stream, host
     transport for the Gram all-reduce and the all-gathers); factors match the single-process oracle.
     nonneg: the NNLS half-sweeps (lockstep + per-row kernels) with the blocking chunk gathers.
     split: ALBEDO_SPLIT_CHUNK=128 sends every row above 128 ratings (the popular repos) through the
-    split-K partial + reduce path inside the solve chunks of each rank.  Then recommendForAllUsers(10)
-    with the users sharded across the ranks: every rank returns every list, bit-exact against the
-    oracle scorer on the fitted factors."""
+    split-K partial + reduce path inside the solve chunks of each rank.  k = 128 runs the c4 bench's
+    kernels sharded: the bf16 rotation of the whole gathered src with the fused pre-split into a
+    buffer of prows() + 1 rows, light16 (pairs and singles), light D = 32 / 64, the wave kernel and
+    split-K partials; k = 256 the NNLS kernels at the c5 rank.  Then recommendForAllUsers(10) with the
+    users sharded across the ranks: every rank returns every list, bit-exact against the oracle scorer
+    on the fitted factors."""
     env = {"ALBEDO_SPLIT_CHUNK": str(split)} if split else None
     out = str(tmp_path / "gpu.npz")
-    res = _launch("gpunn" if nonneg else "gpu", out, world=world, env_extra=env)
-    B, U0, V0 = _problem()
+    res = _launch("gpunn" if nonneg else "gpu", out, world=world, env_extra=env, k=k)
+    B, U0, V0 = _problem(k)
     if split:
         assert np.max(np.diff(B.i_ptr)) > 2 * split  # rows that really take the split-K path
-    U, V = O.fit(B, rank=16, max_iter=3, reg=0.5, alpha=40.0, init_user=U0, init_item=V0, nonnegative=nonneg)
+    if k == 128:  # every light bucket and the wave kernel have rows
+        deg = np.r_[np.diff(B.i_ptr), np.diff(B.u_ptr)]
+        assert all(np.any((deg > lo) & (deg <= hi)) for lo, hi in ((0, 8), (8, 16), (16, 32), (32, 64), (64, 128)))
+    U, V = _fit_ref(B, U0, V0, k, 3, nonneg)
     rel = lambda a, b: np.max(np.abs(a - b)) / np.max(np.abs(b))
     assert rel(res["U"], U) < 1e-3 and rel(res["V"], V) < 1e-3
     ref_ids, ref_sc = O.recommend_for_all(B.user_ids, res["U"], B.item_ids, res["V"], 10)

@@ -52,6 +52,9 @@ for s in "$@"; do
     debug_c1) timeout -k 10 300 python -u tools/debug_c1.py > gpurun_out/debug_c1.log 2>&1; r=$?; echo "debug_c1 rc $r"; [ $r -le 1 ] ;;
     protocol_eu) { timeout -k 10 300 python -u tools/protocol_eu.py main; } > gpurun_out/protocol_eu.log 2>&1 ;;
     factortime)(cd tools/probe && timeout -k 5 120 ./factortime 1000000) > gpurun_out/factortime.txt 2>&1 ;;
+    factortime3)(cd tools/probe && timeout -k 5 120 ./factortime 1000000 && timeout -k 5 120 ./factortime_bgoff 1000000 && timeout -k 5 120 ./factortime_old 1000000) > gpurun_out/factortime3.txt 2>&1 ;;
+    factortime2)(cd tools/probe && timeout -k 5 120 ./factortime 1000000 && timeout -k 5 120 ./factortime_old 1000000) > gpurun_out/factortime2.txt 2>&1 ;;
+    topkph) timeout -k 10 400 python -u tools/topk_phases.py --lib tools/ab/topkph.so --out gpurun_out/topkph.json > gpurun_out/topkph.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
