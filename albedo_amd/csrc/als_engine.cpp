@@ -1508,7 +1508,7 @@ struct TopkPlan {
   int64_t n_chunks = 0, n_super = 0;
   bool prune = false;
   DevBuf d_th, d_keys, d_perm, d_nperm, d_tp, d_tmp, d_dstids, d_VP, d_cfeat, d_supf, d_probe, d_slab, d_G;
-  DevBuf d_src, d_ls, d_li, d_lc, d_need, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp, d_thr, d_sf, d_mask, d_kth;
+  DevBuf d_src, d_ls, d_lc, d_need, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp, d_thr, d_sf, d_mask, d_kth;
 };
 
 // The leading TOPK_M eigenvectors of the dst side's Gram Σ t tᵀ (original basis), fp64 [TOPK_M][KP]:
@@ -1616,8 +1616,7 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int3
   HIPCHK(P.d_src.ensure(nc * 4));
   HIPCHK(P.d_need.ensure(nc * 4));
   if (!P.exact_only) {
-    HIPCHK(P.d_ls.ensure(nc * TOPK_CAP * 4));
-    HIPCHK(P.d_li.ensure(nc * TOPK_CAP * 4));
+    HIPCHK(P.d_ls.ensure(nc * TOPK_CAP * 8));
     HIPCHK(P.d_lc.ensure(nc * 4));
   }
   HIPCHK(hipMemcpyAsync(P.d_src.p, rows, nc * 4, hipMemcpyHostToDevice, c->st));
@@ -1644,8 +1643,7 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int3
   a.tsc = (float)P.tsc;
   a.unscale = (float)(1.0 / (P.ssc * P.tsc));
   a.scaled = (float)(P.ssc * P.tsc);
-  a.lscore = P.d_ls.as<float>();
-  a.lidx = P.d_li.as<int32_t>();
+  a.lent = P.d_ls.as<uint2>();
   a.lcnt = P.d_lc.as<int32_t>();
   a.out_ids = d_oid;
   a.out_scores = d_osc;

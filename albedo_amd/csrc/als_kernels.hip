@@ -866,7 +866,7 @@ __device__ __forceinline__ void light_row(const SolveArgs& a, int j, int d, floa
       bacc[A] = __shfl(A < 4 ? rhs : rhs2, 16 * (A & 3) + i16);
     });
     float xs[NB];
-    const bool notpd = WAVE_CHOL_SOLVE<NB>(acc, bacc, Ks, xs);
+    const bool notpd = wave_chol_solve<NB>(acc, bacc, Ks, xs);
     if (notpd && lane == 0) atomicOr(a.err, 2 | ALBEDO_EF_LIGHT_ACC);
     y = 0.f;  // lane 16A + i holds v[16A + i] = xs[A] (its own slot A = g); y2: v[64 + 16A + i]
 #pragma unroll

@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256, 2) void solve_wave_kernel(SolveArgs a) {
 #endif
   // ---- blocked Cholesky A' = UᵀU on the tiles, RHS alongside (wave_chol.h) -----------------------
   float xs[NQ];
-  const bool notpd = WAVE_CHOL_SOLVE<NQ, true>(acc, bacc, reinterpret_cast<float*>(st), xs);
+  const bool notpd = wave_chol_solve<NQ, true>(acc, bacc, reinterpret_cast<float*>(st), xs);
   WAVE_STAMP(ridx, 2);
   bool nonfinite = false;
 #pragma unroll

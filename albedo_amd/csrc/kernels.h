@@ -163,8 +163,7 @@ struct TopkArgs {
   float ssc, tsc;          // src / dst fp16 scales (powers of two)
   float unscale;           // 1 / (ssc·tsc): exact rescaling of the MFMA scores
   float scaled;            // ssc·tsc
-  float* lscore;           // [n_src][TOPK_CAP] candidate lists (approx score, scan position)
-  int32_t* lidx;
+  uint2* lent;             // [n_src][TOPK_CAP] candidate lists: (approx score bits, scan position) pairs
   int32_t* lcnt;           // [n_src] list lengths
   int32_t* out_ids;        // [n_src][k] raw dst ids
   float* out_scores;       // [n_src][k]

@@ -65,6 +65,28 @@ typedef __attribute__((address_space(1))) const void* tk_glb_vp;
 __device__ __forceinline__ bool tk_before(float s1, int i1, float s2, int i2) {
   return s1 > s2 || (s1 == s2 && (unsigned)i1 < (unsigned)i2);
 }
+// The value of lane l ^ JJ (JJ < 64) without the LDS crossbar (a __shfl_xor is a ds_bpermute, ~100+
+// cycles of latency, and a compaction's bitonic sort is 27 dependent exchange steps): DPP quad
+// permutes for 1 and 2, row_ror:8 for 8, two row shifts for 4, v_permlane16/32_swap for 16 / 32.
+template <int JJ>
+__device__ __forceinline__ int xor_lane(int v, int lane) {
+  if constexpr (JJ == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  else if constexpr (JJ == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  else if constexpr (JJ == 4) {
+    const int up = __builtin_amdgcn_mov_dpp(v, 0x104, 0xF, 0xF, false);  // row_shl:4: lane i + 4
+    const int dn = __builtin_amdgcn_mov_dpp(v, 0x114, 0xF, 0xF, false);  // row_shr:4: lane i - 4
+    return (lane & 4) ? dn : up;
+  } else if constexpr (JJ == 8) return __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  else if constexpr (JJ == 16) {
+    const auto p = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)((lane & 16) ? p[0] : p[1]);
+  } else {
+    static_assert(JJ == 32, "xor distance");
+    const auto p = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)((lane & 32) ? p[0] : p[1]);
+  }
+}
+
 template <int NPL, int K, int JJ>
 __device__ __forceinline__ void bitonic_step(float (&sc)[NPL], int (&ix)[NPL], int lane) {
   if constexpr (JJ >= 64) {
@@ -81,8 +103,8 @@ __device__ __forceinline__ void bitonic_step(float (&sc)[NPL], int (&ix)[NPL], i
   } else {
     static_for<0, NPL>([&](auto hc) {
       constexpr int h = decltype(hc)::value;
-      const float os = __shfl_xor(sc[h], JJ);
-      const int oi = __shfl_xor(ix[h], JJ);
+      const float os = __int_as_float(xor_lane<JJ>(__float_as_int(sc[h]), lane));
+      const int oi = xor_lane<JJ>(ix[h], lane);
       const int e = lane + 64 * h;
       const bool lower = (lane & JJ) == 0;
       const bool up = (e & K) == 0;
@@ -123,15 +145,21 @@ struct TkScan {
   static constexpr int CH = CB / RB;             // dst rows per chunk
   static constexpr int NJ = CH / 16;             // 16-row tiles per chunk
   static constexpr int NQ = KP / 32;             // 32-deep MFMA steps per tile
-  static constexpr int NSTG = G >= 4 ? 6 : 4;    // ring depth (chunks)
+  // G <= 4: two workgroups per CU (r05; at one per CU every wave is alone on its SIMD and the scan's
+  // DMA, LDS, barrier and list latencies are all exposed): a 4-chunk ring, the first 2048 mask words in
+  // LDS (the rest read from global memory by the mask window) -- 75 KB per workgroup.  G = 8 needs
+  // more than 256 registers per lane (the AGPRs of a wave alone on its SIMD): one per CU, 6 chunks.
+  // The src features live in registers (r04: LDS).
+  static constexpr int OCC = G <= 4 ? 2 : 1;     // workgroups per CU
+  static constexpr int NSTG = OCC == 2 ? 4 : 6;  // ring depth (chunks)
   static constexpr int SLOT = CB + 4 * 64;       // + each wave's copy of the chunk's bound box
   static constexpr int RING = NSTG * SLOT;
   static constexpr int RWG = 64 * G;             // src rows per workgroup (16·G per wave)
   static constexpr int DPW = CB / 1024 / 4;      // 1-KiB row DMAs per wave per chunk
   static constexpr int NVM = DPW + 1;            // DMA instructions per wave per chunk (rows + box)
-  static constexpr int MASKW = 8192;             // mask words kept in LDS (chunks 0 .. 262143)
-  static constexpr int LDS = RING + RWG * 4 + RWG * TOPK_SF * 4 + MASKW * 4;
-  static_assert(LDS <= 160 * 1024, "LDS budget");
+  static constexpr int MASKW = OCC == 2 ? 2048 : 8192;  // mask words kept in LDS
+  static constexpr int LDS = RING + RWG * 4 + MASKW * 4;
+  static_assert(OCC * LDS <= 160 * 1024, "LDS budget");
 };
 template <int KP>
 __host__ __device__ constexpr int topk_chunk_rows_dev() { return TkScan<KP, 2>::CH; }
@@ -147,6 +175,9 @@ __device__ __forceinline__ float agent_load(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ int agent_load(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t agent_load64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -187,7 +218,7 @@ __device__ unsigned long long g_tk_ph[16];  // [0..7] cycles per phase summed ov
 #endif
 
 template <int KP, int G>
-__global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
+__global__ __launch_bounds__(256, (TkScan<KP, G>::OCC)) void topk_scan_kernel(TopkArgs a) {
   using C = TkScan<KP, G>;
   constexpr int NQ = C::NQ, NJ = C::NJ, RB = C::RB, CAP = TOPK_CAP, SF = TOPK_SF;
   // a list is compacted to its best 64 once it holds more than TRIG (<= TRIG + 16 <= 64·NSC entries):
@@ -196,8 +227,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
   static_assert(TRIG + 16 <= 64 * NSC && TRIG + 16 <= CAP && TRIG + 16 <= 255, "compaction width, byte counters");
   extern __shared__ __attribute__((aligned(16))) char lds[];  // one LDS object (glds pipelining)
   float* s_thr = reinterpret_cast<float*>(lds + C::RING);  // [RWG] thresholds (unscaled)
-  float* s_sf = s_thr + C::RWG;                              // [RWG][SF] src features
-  uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_sf + C::RWG * SF);  // [MASKW] this workgroup's mask
+  uint32_t* s_mask = reinterpret_cast<uint32_t*>(s_thr + C::RWG);  // [MASKW] this workgroup's mask
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i16 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t rb0 = (int64_t)blockIdx.x * C::RWG;  // first src-list position of the workgroup
@@ -228,10 +258,11 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
     }
     if (g == 0) s_thr[wr0 + 16 * gi + i16] = srow < 0 ? INFINITY : (a.thr0 ? a.thr0[si] : -INFINITY);
   }
-  for (int e = tid; e < C::RWG * SF; e += 256) {
-    const int64_t si = rb0 + e / SF;
-    s_sf[e] = si < a.n_src && a.sfeat ? a.sfeat[rb0 * SF + e] : 0.f;
-  }
+  // src feature f of workgroup row w (global memory: read at setup only)
+  auto sfeat = [&](int w, int f) -> float {
+    const int64_t si = rb0 + w;
+    return si < a.n_src && a.sfeat ? a.sfeat[si * SF + f] : 0.f;
+  };
   const uint32_t* mw = a.mask ? a.mask + (int64_t)blockIdx.x * a.mask_words : nullptr;
   const int64_t mlds = mw ? (a.mask_words < C::MASKW ? a.mask_words : C::MASKW) : 0;
   for (int64_t w = tid; w < mlds; w += 256) s_mask[w] = mw[w];
@@ -246,26 +277,39 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
       const int wrow = wr0 + 16 * gi + 4 * g + r;
       const float t0 = s_thr[wrow];
       nthr[gi][r] = t0 == INFINITY ? -INFINITY
-                  : t0 == -INFINITY ? 1.01f * s_sf[wrow * SF + TOPK_M + 2] * a.ssc * tmax_sc + 1.f : -(t0 * a.scaled);
+                  : t0 == -INFINITY ? 1.01f * sfeat(wrow, TOPK_M + 2) * a.ssc * tmax_sc + 1.f : -(t0 * a.scaled);
     }
 
-  // the chunk sequence: the set bits of this workgroup's mask (every chunk without one), ascending;
-  // the mask words come from LDS (beyond MASKW words: global memory)
-  auto next_chunk = [&](int64_t x) -> int64_t {  // smallest chunk > x in the sequence (nch: none)
+  // the chunk sequence: the set bits of this workgroup's mask (every chunk without one), ascending.
+  // A window of 64 mask words (2048 chunks) is held in one VGPR (lane l: word base + l, from LDS;
+  // beyond MASKW words from global memory): the next set bit is a ballot + ctz, and a new window is
+  // read only when the walk leaves the current one (r04 read one LDS word per call and per empty
+  // word: 8.5 % of the scan's wave-cycles).  Two cursors (DMA issue, consume) keep a window each.
+  struct MaskWin { int64_t base; uint32_t word; };
+  auto next_chunk = [&](int64_t x, MaskWin& mwin) -> int64_t {  // smallest chunk > x in the sequence (nch: none)
     int64_t c = x + 1;
     if (!mw) return c < nch ? c : nch;
     while (c < nch) {
-      const int64_t w = c >> 5;
-      const uint32_t word = w < mlds ? s_mask[w] : mw[w];
-      const uint32_t bits = (uint32_t)__builtin_amdgcn_readfirstlane((int)word) >> (c & 31);
-      if (bits) {
-        c += __builtin_ctz(bits);
+      const int64_t w0 = c >> 5;
+      if (w0 < mwin.base || w0 >= mwin.base + 64) {
+        mwin.base = w0;
+        const int64_t w = w0 + lane;
+        mwin.word = w < mlds ? s_mask[w] : (w < a.mask_words ? mw[w] : 0u);
+      }
+      const int rel = (int)(w0 - mwin.base);
+      const uint32_t word = lane < rel ? 0u : (lane == rel ? mwin.word & (~0u << (c & 31)) : mwin.word);
+      const uint64_t nz = __ballot(word != 0u);
+      if (nz) {
+        const int L = __builtin_ctzll(nz);
+        const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)word, L);
+        c = ((mwin.base + L) << 5) + __builtin_ctz(bits);
         return c < nch ? c : nch;
       }
-      c = (w + 1) << 5;
+      c = (mwin.base + 64) << 5;
     }
     return nch;
   };
+  MaskWin win_iss{-((int64_t)1 << 40), 0u}, win_use{-((int64_t)1 << 40), 0u};
 
   // DMA of chunk c into ring slot `slot`: the wave's DPW KiB of rows (source addresses carry the
   // unit swizzle, the LDS image is lane-linear), then the wave's own copy of the chunk's bound box
@@ -287,13 +331,25 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
   };
   int64_t c_iss = -1, n_iss = 0;
   for (int u = 0; u < C::NSTG - 1; ++u) {
-    c_iss = next_chunk(c_iss);
+    c_iss = next_chunk(c_iss, win_iss);
     if (c_iss < nch) {
       dma(c_iss, u);
       ++n_iss;
     }
   }
 
+  // the bound test's src features (s_P, ‖s_⊥‖, margin) and thresholds of this lane's rows
+  // lane + 64h in registers (r04 read them from LDS for every chunk); the thresholds are re-read after
+  // a compaction raised some
+  constexpr int BH = (16 * G + 63) / 64;
+  float bsf[BH][TOPK_M + 2], bthr[BH];
+#pragma unroll
+  for (int h = 0; h < BH; ++h) {
+    const int rr = lane + 64 * h < 16 * G ? lane + 64 * h : 0;
+#pragma unroll
+    for (int f = 0; f < TOPK_M + 2; ++f) bsf[h][f] = sfeat(wr0 + rr, f);
+    bthr[h] = lane + 64 * h < 16 * G ? s_thr[wr0 + rr] : INFINITY;
+  }
   TKPH_T0();
   // candidates of one 16-row tile (dst positions jt .. jt+15).  Slots come from a ballot prefix count
   // over the 16 lanes of a row's group; list lengths live in registers, one byte per row (cntp[gi]
@@ -324,8 +380,8 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
           const int cnt = (int)((cntp[gi] >> (8 * r)) & 0xffu);
           if (p) {
             const int64_t li = (rb0 + wrow) * CAP + cnt + __popc(mg & below);
-            a.lscore[li] = (acc[gi][r] - nthr[gi][r]) * a.unscale;  // score = acc + threshold
-            a.lidx[li] = (int)dj;
+            // score = acc + threshold; (score, position) in one 8-byte store
+            a.lent[li] = uint2{__float_as_uint((acc[gi][r] - nthr[gi][r]) * a.unscale), (uint32_t)dj};
           }
           const int ncnt = cnt + __popc(mg);
           cntp[gi] += (uint32_t)__popc(mg) << (8 * r);
@@ -368,12 +424,13 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
 #pragma unroll
       for (int h = 0; h < NSC; ++h) {
         const int e = lane + 64 * h;
-        s2[h] = e < cnt ? agent_load(a.lscore + lb + e) : -INFINITY;
-        i2[h] = e < cnt ? agent_load(a.lidx + lb + e) : -1;
+        const uint64_t v = e < cnt ? agent_load64(reinterpret_cast<const uint64_t*>(a.lent + lb + e))
+                                   : ((uint64_t)0xFFFFFFFFu << 32) | __float_as_uint(-INFINITY);
+        s2[h] = __uint_as_float((uint32_t)v);
+        i2[h] = (int)(uint32_t)(v >> 32);
       }
       wave_bitonic<NSC>(s2, i2);
-      a.lscore[lb + lane] = s2[0];
-      a.lidx[lb + lane] = i2[0];
+      a.lent[lb + lane] = uint2{__float_as_uint(s2[0]), (uint32_t)i2[0]};
       const float tkt = rdlane(s2[0], a.kt - 1);  // the running kt-th best becomes the threshold
       if (lane == 0) s_thr[wr0 + wl] = tkt;
     }
@@ -390,11 +447,14 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
           cntp[gi] = (cntp[gi] & ~(0xffu << (8 * r))) | (64u << (8 * r));
         }
       }
+#pragma unroll
+    for (int h = 0; h < BH; ++h)
+      if (lane + 64 * h < 16 * G) bthr[h] = s_thr[wr0 + lane + 64 * h];
     TKPH(4);  // compaction loads + sorts + stores
   };
 
   int64_t it = 0, n_scored = 0;  // chunk iterations; chunks this wave scored (its `need` held)
-  for (int64_t c = next_chunk(-1); c < nch; c = next_chunk(c), ++it) {
+  for (int64_t c = next_chunk(-1, win_use); c < nch; c = next_chunk(c, win_use), ++it) {
     TKPH(5);  // next_chunk (mask walk)
     // this wave's DMAs of chunk c have landed (in-order VM counter; later list stores only make the
     // wait stricter), then one barrier publishes every wave's part and retires the previous slot
@@ -403,7 +463,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (c_iss < nch) {
-      c_iss = next_chunk(c_iss);
+      c_iss = next_chunk(c_iss, win_iss);
       if (c_iss < nch) {
         dma(c_iss, (int)((it + C::NSTG - 1) % C::NSTG));
         ++n_iss;
@@ -424,13 +484,7 @@ __global__ __launch_bounds__(256, 1) void topk_scan_kernel(TopkArgs a) {
         for (int e = 0; e < 4; ++e) cfr[f + e] = v[e];
       }
 #pragma unroll
-      for (int h = 0; h < (16 * G + 63) / 64; ++h) {
-        const int rr = lane + 64 * h;
-        if (rr < 16 * G) {
-          const float* srf = s_sf + (wr0 + rr) * SF;
-          need |= tk_bound(srf, cfr) + srf[TOPK_M + 1] >= s_thr[wr0 + rr];
-        }
-      }
+      for (int h = 0; h < BH; ++h) need |= tk_bound(bsf[h], cfr) + bsf[h][TOPK_M + 1] >= bthr[h];
     }
     TKPH(1);  // chunk bound test
     if (!__any(need)) continue;
@@ -492,8 +546,9 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
 #pragma unroll
   for (int h = 0; h < NS; ++h) {
     const int e = lane + 64 * h;
-    s2[h] = e < cnt ? a.lscore[si * CAP + e] : -INFINITY;
-    i2[h] = e < cnt ? a.lidx[si * CAP + e] : -1;
+    const uint2 v = e < cnt ? a.lent[si * CAP + e] : uint2{__float_as_uint(-INFINITY), 0xFFFFFFFFu};
+    s2[h] = __uint_as_float(v.x);
+    i2[h] = (int)v.y;
   }
   wave_bitonic<NS>(s2, i2);
   const float t = rdlane(s2[0], a.kt - 1);  // the kt-th approximate score (-inf when fewer)
@@ -1080,6 +1135,11 @@ hipError_t launch_scan(const TopkArgs& a, hipStream_t s) {
 // that still gives every CU two workgroups, down to G = 2
 int topk_rows_per_workgroup(int KP, int64_t n_src, int n_cu) {
   int gmax = KP <= 128 ? 8 : 4;
+  static const int gcap = [] {  // ALBEDO_TOPK_GMAX: A/B knob (2, 4 or 8)
+    const char* e = std::getenv("ALBEDO_TOPK_GMAX");
+    return e && *e ? std::atoi(e) : 8;
+  }();
+  gmax = std::min(gmax, std::max(2, gcap));
   for (int G = gmax; G > 2; G /= 2)
     if (n_src >= (int64_t)2 * n_cu * 64 * G) return 64 * G;
   return 128;

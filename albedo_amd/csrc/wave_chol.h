@@ -214,253 +214,4 @@ __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2],
   return notpd;
 }
 
-// ---- look-ahead variant (r05) ------------------------------------------------------------------
-// The same factorisation and the same roundings as wave_chol_solve (bit-identical x), scheduled so
-// that the matrix core works while the VALU factors.  Per panel jb only a short chain is serial:
-//   U(jb, jb+1) = L⁻¹_jb T(jb, jb+1)  ->  split  ->  T(jb+1, jb+1) -= UᵀU  ->  chol16 + L⁻¹ of tile jb+1;
-// the rest of panel jb -- U(jb, I) for I >= jb+2, their splits and the trailing updates T(M, I),
-// M >= jb+1, I >= jb+2 -- is issued a few instructions at a time between the 32 dependent steps of
-// that chol16 + L⁻¹ (a compile-time schedule, pinned by scheduling barriers), so its MFMAs drain
-// behind the VALU chain instead of in front of it (an in-order wave that issues a burst of MFMAs
-// stalls until the matrix pipe takes each one).  The right-hand side leaves the panel loop: the
-// forward substitution y = L⁻¹b runs after the factorisation on the kept U tiles, with the same
-// operations in the same order as wave_chol_solve's per-panel RHS.
-
-// background item i of panel jb (NQ blocks): kind 0 = issue U(jb, a); 1 = SPLIT: start row a (split
-// U(jb, a) into the row operand); 2 = update T(a, b) -= U(jb, a)ᵀ U(jb, b) (SPLIT: U(jb, b) split on
-// the spot: one split per update instead of a kept split per block, which spilled).  Order: every U
-// issue, then row by row M = jb+1 .. the updates T(M, I), I >= max(M, jb+2).
-struct BgItem { int kind, a, b; };
-template <bool SPLIT>
-__host__ __device__ constexpr int bg_count(int nq, int jb) {
-  int n = nq - jb - 2 > 0 ? nq - jb - 2 : 0;
-  for (int M = jb + 1; M < nq; ++M) {
-    const int i0 = M > jb + 2 ? M : jb + 2;
-    if (i0 >= nq) continue;
-    n += (SPLIT && M > jb + 1 ? 1 : 0) + (nq - i0);
-  }
-  return n;
-}
-template <bool SPLIT>
-__host__ __device__ constexpr BgItem bg_item(int nq, int jb, int i) {
-  const int nu = nq - jb - 2 > 0 ? nq - jb - 2 : 0;
-  if (i < nu) return BgItem{0, jb + 2 + i, 0};
-  i -= nu;
-  for (int M = jb + 1; M < nq; ++M) {
-    const int i0 = M > jb + 2 ? M : jb + 2;
-    if (i0 >= nq) continue;
-    if (SPLIT && M > jb + 1) {
-      if (i == 0) return BgItem{1, M, 0};
-      --i;
-    }
-    if (i < nq - i0) return BgItem{2, M, i0 + i};
-    i -= nq - i0;
-  }
-  return BgItem{-1, 0, 0};
-}
-// the diagonal factorisation's 32 steps (16 chol16 pivots, 16 L⁻¹ columns) carry the items evenly
-template <bool SPLIT>
-__host__ __device__ constexpr int bg_step(int nq, int jb, int i) {
-  const int n = bg_count<SPLIT>(nq, jb);
-  return n == 0 ? 0 : (i * 32) / n;
-}
-
-// Diagonal tile JB of acc -> chol16 -> its L⁻¹ in the A-operand layout (returned, and kept in
-// s_linv[JB]); bg(step) runs between the dependent steps (step 0..15: after pivot `step`, 16..31:
-// after L⁻¹ column step - 16).
-template <int NQ, int JB, typename BG>
-__device__ __forceinline__ f32x4 wave_diag_factor(f32x4 (&acc)[NQ * (NQ + 1) / 2], float* scr, bool& notpd, BG&& bg) {
-  const int lane = threadIdx.x & 63, q = lane >> 4, i16 = lane & 15;
-  constexpr int td = tix(JB, JB, NQ);
-  f32x4* s_linv = reinterpret_cast<f32x4*>(scr + WCHOL_SCR);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) scr[(4 * q + r) * WCHOL_RS + i16] = acc[td][r];
-  WAVE_LDS_SYNC();
-  float rr[16];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const f32x4 v = ld4(scr + WCHOL_RS * i16 + 4 * u);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) rr[4 * u + e] = v[e];
-  }
-  // chol16 (device_common.h) with the background hook after every pivot
-  float dg = 1.f;
-  {
-    bool np = false;
-    float d0 = 0.f;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) d0 = (i16 == c) ? rr[c] : d0;
-    static_for<0, 16>([&](auto cc) {
-      constexpr int c = decltype(cc)::value;
-      if (i16 == c && !(rr[c] > d0 * 4.76837158e-07f)) np = true;
-      const float piv = bc16_after_asm<c>(rr[c]);
-      const float inv = frsq(piv), sq = piv * inv;
-      rr[c] = (i16 == c) ? sq : rr[c] * inv;
-      dg = (i16 == c) ? inv : dg;
-      static_for<c + 1, 16>([&](auto mm) {
-        constexpr int m = decltype(mm)::value;
-        fnmac_bc16<m, m == c + 1>(rr[m], rr[c], rr[c]);
-      });
-      bg(std::integral_constant<int, c>{});
-    });
-    notpd |= __any(np);
-  }
-  asm volatile("s_nop 1"
-               : "+v"(rr[0]), "+v"(rr[1]), "+v"(rr[2]), "+v"(rr[3]), "+v"(rr[4]), "+v"(rr[5]), "+v"(rr[6]),
-                 "+v"(rr[7]), "+v"(rr[8]), "+v"(rr[9]), "+v"(rr[10]), "+v"(rr[11]), "+v"(rr[12]),
-                 "+v"(rr[13]), "+v"(rr[14]), "+v"(rr[15]), "+v"(dg));
-  float x[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) x[r] = (i16 == r) ? 1.f : 0.f;
-  static_for<0, 16>([&](auto MM) {
-    constexpr int m = decltype(MM)::value;
-    x[m] *= bc16_after_asm<m>(dg);
-    static_for<m + 1, 16>([&](auto RR) {
-      constexpr int r = decltype(RR)::value;
-      fnmac_bc16<r, false>(x[r], rr[m], x[m]);
-    });
-    bg(std::integral_constant<int, 16 + m>{});
-  });
-  if (q == 0) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) scr[WCHOL_IMG + WCHOL_RS * r + i16] = x[r];
-  }
-  WAVE_LDS_SYNC();
-  const f32x4 lv = ld4(scr + WCHOL_IMG + WCHOL_RS * i16 + 4 * q);
-  s_linv[JB * 64 + lane] = lv;
-  return lv;
-}
-
-template <int NQ, bool SPLIT = false>
-__device__ __forceinline__ bool wave_chol_solve_la(f32x4 (&acc)[NQ * (NQ + 1) / 2], float (&bacc)[NQ], float* scr,
-                                                   float (&xs)[NQ]) {
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  const int lane = threadIdx.x & 63, q = lane >> 4, i16 = lane & 15;
-  f32x4* s_linv = reinterpret_cast<f32x4*>(scr + WCHOL_SCR);
-  bool notpd = false;
-  WCHOL_T0();
-  f32x4 lv = wave_diag_factor<NQ, 0>(acc, scr, notpd, [](auto) {});
-  WCHOL_PH(1);
-  static_for<0, NQ - 1>([&](auto JB) {
-    constexpr int jb = decltype(JB)::value;
-    const f32x4 lp = lv;  // L⁻¹ of panel jb (the background's U products need it)
-    auto uprod = [&](auto II) {  // U(jb, I) = L⁻¹ T(jb, I)
-      constexpr int t = tix(jb, decltype(II)::value, NQ);
-      f32x4 u = zero4();
-#pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) u = mfma4(lp[s2], acc[t][s2], u);
-      acc[t] = u;
-    };
-    f16x8 ubm;  // SPLIT: [hi | lo] of U(jb, M) for the current row M of the background updates
-    auto upd = [&](auto MM, auto II) {  // T(M, I) -= U(jb, M)ᵀ U(jb, I)
-      constexpr int M = decltype(MM)::value, I = decltype(II)::value, t = tix(M, I, NQ);
-      if constexpr (SPLIT) {
-        const f16x8 ubi = I == M ? ubm : split_hilo4(acc[tix(jb, I, NQ)]);
-        const u32x4 w = __builtin_bit_cast(u32x4, ubm) ^ 0x80008000u;  // -hi, -lo
-        const f16x8 a1 = __builtin_bit_cast(f16x8, (u32x4{w[0], w[1], w[0], w[1]}));  // [-hi | -hi]
-        const f16x8 a2 = __builtin_bit_cast(f16x8, (u32x4{w[2], w[3], 0u, 0u}));      // [-lo | 0]
-        acc[t] = mfma_h(a1, ubi, acc[t]);
-        acc[t] = mfma_h(a2, ubi, acc[t]);
-      } else {
-        constexpr int tm = tix(jb, M, NQ), ti = tix(jb, I, NQ);
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) acc[t] = mfma4(-acc[tm][s2], acc[ti][s2], acc[t]);
-      }
-    };
-    // the serial chain: U(jb, jb+1), then the next diagonal tile's update
-    uprod(std::integral_constant<int, jb + 1>{});
-    if constexpr (SPLIT) ubm = split_hilo4(acc[tix(jb, jb + 1, NQ)]);
-    upd(std::integral_constant<int, jb + 1>{}, std::integral_constant<int, jb + 1>{});
-    WCHOL_PH(3);
-    // the rest of the panel in the background of the next diagonal factorisation
-    constexpr int NBG = bg_count<SPLIT>(NQ, jb);
-    auto bg = [&](auto S) {
-      constexpr int step = decltype(S)::value;
-      static_for<0, NBG>([&](auto Ii) {
-        constexpr int i = decltype(Ii)::value;
-        if constexpr (bg_step<SPLIT>(NQ, jb, i) == step) {
-          constexpr BgItem it = bg_item<SPLIT>(NQ, jb, i);
-          if constexpr (it.kind == 0) uprod(std::integral_constant<int, it.a>{});
-          else if constexpr (it.kind == 1) {
-            if constexpr (SPLIT) ubm = split_hilo4(acc[tix(jb, it.a, NQ)]);
-          } else if constexpr (it.kind == 2) {
-            upd(std::integral_constant<int, it.a>{}, std::integral_constant<int, it.b>{});
-          }
-        }
-      });
-      __builtin_amdgcn_sched_barrier(0);
-    };
-#ifdef ALBEDO_BG_OFF
-    lv = wave_diag_factor<NQ, jb + 1>(acc, scr, notpd, [](auto) {});
-    static_for<0, 32>([&](auto S) { bg(S); });
-#else
-    lv = wave_diag_factor<NQ, jb + 1>(acc, scr, notpd, bg);
-#endif
-    WCHOL_PH(1);
-  });
-
-  // ---- forward substitution: y_jb = L_jb⁻¹ b_jb, then b_M -= U(jb, M)ᵀ y_jb ----------------------
-  static_for<0, NQ>([&](auto JB) {
-    constexpr int jb = decltype(JB)::value;
-    if (q == 0) scr[WCHOL_IMG + i16] = bacc[jb];
-    WAVE_LDS_SYNC();
-    const f32x4 bt = ld4(scr + WCHOL_IMG + 4 * q);  // lane i + 16q: b_jb[4q .. 4q+3] (the MFMA k layout)
-    const f32x4 lj = s_linv[jb * 64 + lane];
-    float yp = 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) yp = fmaf(lj[s], bt[s], yp);
-    yp = rows4_sum(yp);
-    bacc[jb] = yp;
-    if constexpr (jb + 1 < NQ) {
-      WAVE_LDS_SYNC();  // bt read before the scratch is rewritten
-      if (q == 0) scr[WCHOL_IMG + i16] = yp;
-      WAVE_LDS_SYNC();
-      const f32x4 y4 = ld4(scr + WCHOL_IMG + 4 * q);
-      static_for<jb + 1, NQ>([&](auto MM) {
-        constexpr int M = decltype(MM)::value, t = tix(jb, M, NQ);
-        float pv = 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pv = fmaf(acc[t][r], y4[r], pv);
-        bacc[M] -= rows4_sum(pv);
-      });
-    }
-    WAVE_LDS_SYNC();
-  });
-  WCHOL_PH(4);
-
-  // ---- back substitution: x_jb = L_jb⁻ᵀ (y_jb - Σ_{M > jb} U(jb, M) x_M) (as wave_chol_solve) ----
-  static_for<0, NQ>([&](auto KK) {
-    constexpr int jb = NQ - 1 - decltype(KK)::value;
-    float pr[4] = {0.f, 0.f, 0.f, 0.f};
-    static_for<jb + 1, NQ>([&](auto MM) {
-      constexpr int M = decltype(MM)::value, t = tix(jb, M, NQ);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) pr[r] = fmaf(acc[t][r], xs[M], pr[r]);
-    });
-    float tq[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) tq[r] = sum16_last(pr[r]);
-    const f32x4 lvb = s_linv[jb * 64 + lane];
-    if (i16 == 15) *reinterpret_cast<f32x4*>(scr + 4 * q) = f32x4{tq[0], tq[1], tq[2], tq[3]};
-    WAVE_LDS_SYNC();
-    const float ti = bacc[jb] - scr[i16];
-    float xq[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) xq[s] = sum16_last(lvb[s] * ti);
-    if (i16 == 15) *reinterpret_cast<f32x4*>(scr + 16 + 4 * q) = f32x4{xq[0], xq[1], xq[2], xq[3]};
-    WAVE_LDS_SYNC();
-    xs[jb] = scr[16 + i16];
-  });
-  WCHOL_PH(6);
-  WCHOL_OUT();
-  return notpd;
-}
-
-// the factorisation the kernels call (ALBEDO_WAVE_CHOL_LA: the look-ahead schedule, for A/B builds)
-#ifdef ALBEDO_WAVE_CHOL_LA
-#define WAVE_CHOL_SOLVE wave_chol_solve_la
-#else
-#define WAVE_CHOL_SOLVE wave_chol_solve
-#endif
-
 }  // namespace albedo

@@ -39,6 +39,8 @@ for s in "$@"; do
     c1p) timeout -k 10 900 python -u tools/c1p_job.py --out gpurun_out/c1p_job.json > gpurun_out/c1p_job.log 2>&1 ;;
     tests_eig) timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "device_eigensolver or half_sweep_ranks or orthogonal" > gpurun_out/tests_eig.log 2>&1 ;;
     pmc_topk4) timeout -k 10 600 tools/pmc_topk4.sh r04 > gpurun_out/pmc_topk4.log 2>&1 ;;
+    bench_topk_g4) ALBEDO_TOPK_GMAX=4 timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk_g4.json 2> gpurun_out/bench_topk_g4.err ;;
+    topkph_g4) ALBEDO_TOPK_GMAX=4 timeout -k 10 400 python -u tools/topk_phases.py --lib tools/ab/topkph.so --out gpurun_out/topkph_g4.json > gpurun_out/topkph_g4.log 2>&1 ;;
     bench_topk) timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk.json 2> gpurun_out/bench_topk.err ;;
     bench_c4q) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 > gpurun_out/bench_c4q.json 2> gpurun_out/bench_c4q.err ;;
     bench_c4q_l*) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 --light ${s#bench_c4q_l} > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
@@ -52,8 +54,7 @@ for s in "$@"; do
     debug_c1) timeout -k 10 300 python -u tools/debug_c1.py > gpurun_out/debug_c1.log 2>&1; r=$?; echo "debug_c1 rc $r"; [ $r -le 1 ] ;;
     protocol_eu) { timeout -k 10 300 python -u tools/protocol_eu.py main; } > gpurun_out/protocol_eu.log 2>&1 ;;
     factortime)(cd tools/probe && timeout -k 5 120 ./factortime 1000000) > gpurun_out/factortime.txt 2>&1 ;;
-    factortime3)(cd tools/probe && timeout -k 5 120 ./factortime 1000000 && timeout -k 5 120 ./factortime_bgoff 1000000 && timeout -k 5 120 ./factortime_old 1000000) > gpurun_out/factortime3.txt 2>&1 ;;
-    factortime2)(cd tools/probe && timeout -k 5 120 ./factortime 1000000 && timeout -k 5 120 ./factortime_old 1000000) > gpurun_out/factortime2.txt 2>&1 ;;
+    prot_*) n=${s#prot_}; { ALBEDO_ALS_LIB=$PWD/tools/ab/$n.so timeout -k 10 300 python -u tools/protocol_eu.py $n; } > gpurun_out/prot_$n.log 2>&1 ;;
     topkph) timeout -k 10 400 python -u tools/topk_phases.py --lib tools/ab/topkph.so --out gpurun_out/topkph.json > gpurun_out/topkph.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
