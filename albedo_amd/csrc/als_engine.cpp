@@ -177,7 +177,16 @@ struct als_ctx {
   // [3] exact rescans; [4] scan flops (2·KP per src x dst pair the scan's waves scored)
   double topk_ms[5] = {0, 0, 0, 0, 0};
   hipEvent_t evt[5] = {};
-  std::vector<int32_t> last_rescan;  // src ids the last als_recommend sent to the exact rescan
+  // src ids the last als_recommend / als_evaluate_ndcg sent to the exact rescan, built on demand
+  // (als_topk_last_rescan) from the device flags of that call: position p of the call's rows was
+  // rescanned when d_last_need[p] != 0; its src row is p (last_rows_dense) or last_rows[p]
+  mutable std::vector<int32_t> last_rescan;
+  DevBuf d_last_need;
+  int64_t last_need_n = 0;
+  std::vector<int32_t> last_rows;
+  mutable bool last_rescan_ready = true;
+  bool last_rows_dense = false;
+  int last_src = 0;
   int split_len = 0;             // ratings per split-K chunk (0: no split)
   int slab_blocks = 0;
   hipEvent_t ev[8] = {};
@@ -836,6 +845,57 @@ int heavy_launches(als_ctx* c, const Side& T, SolveArgs a, int64_t h0, int64_t h
 
 bool use_wave_kernel(const als_ctx* c) { return c->KP <= 128; }
 
+// After a failed solve: what the half's inputs and outputs held (non-finite counts, first bad index,
+// max |value|), so a failure that does not repeat still names where it started
+std::string failure_diag(als_ctx* c, const Side& S, const Side& T, int64_t ns, const void* zhl) {
+  const int KP = c->KP;
+  struct Item {
+    const char* name;
+    const void* p;
+    int64_t n;
+    bool f16;
+  } items[] = {{"src X", S.d_X.p, S.own_n * KP, false},
+               {"src Z", S.d_Z.p, ns * KP, false},
+               {"Z zero row", S.d_Z.as<float>() + S.prows() * KP, KP, false},
+               {"Zhl", zhl, zhl ? (S.prows() + 1) * KP * 2 : 0, true},
+               {"lam", c->d_lam.p, KP, false},
+               {"colscale", c->d_cs.p, KP, false},
+               {"dst X", T.d_X.p, T.own_n * KP, false}};
+  const int ni = (int)(sizeof(items) / sizeof(items[0]));
+  DevBuf out;
+  std::vector<unsigned long long> h((size_t)ni * 3, 0ull);
+  for (int i = 0; i < ni; ++i) h[(size_t)i * 3 + 1] = ~0ull;
+  if (out.ensure(h.size() * 8) != hipSuccess ||
+      hipMemcpyAsync(out.p, h.data(), h.size() * 8, hipMemcpyHostToDevice, c->st) != hipSuccess)
+    return " [diagnostics unavailable]";
+  for (int i = 0; i < ni; ++i)
+    if (items[i].p && launch_diag_scan(items[i].p, items[i].n, items[i].f16, out.as<unsigned long long>() + 3 * i, c->st) != hipSuccess)
+      return " [diagnostics unavailable]";
+  std::vector<float> lam(KP), cs(KP);
+  if (hipMemcpyAsync(h.data(), out.p, h.size() * 8, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
+      hipMemcpyAsync(lam.data(), c->d_lam.p, KP * 4, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
+      hipMemcpyAsync(cs.data(), c->d_cs.p, KP * 4, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
+      hipStreamSynchronize(c->st) != hipSuccess)
+    return " [diagnostics unavailable]";
+  std::string r = " [";
+  char buf[160];
+  for (int i = 0; i < ni; ++i) {
+    if (!items[i].p) continue;
+    const unsigned mx = (unsigned)h[(size_t)i * 3 + 2];
+    float fmx;
+    std::memcpy(&fmx, &mx, 4);
+    if (h[(size_t)i * 3])
+      std::snprintf(buf, sizeof buf, "%s: %llu non-finite (first at %llu, row %llu), max %.3g; ", items[i].name,
+                    h[(size_t)i * 3], h[(size_t)i * 3 + 1], h[(size_t)i * 3 + 1] / (items[i].f16 ? 2 * KP : KP), fmx);
+    else std::snprintf(buf, sizeof buf, "%s: finite, max %.3g; ", items[i].name, fmx);
+    r += buf;
+  }
+  const auto lm = std::minmax_element(lam.begin(), lam.begin() + c->p.rank);
+  const auto cm = std::minmax_element(cs.begin(), cs.begin() + c->p.rank);
+  std::snprintf(buf, sizeof buf, "lam %.4g..%.4g, colscale %.4g..%.4g]", *lm.first, *lm.second, *cm.first, *cm.second);
+  return r + buf;
+}
+
 int half_sweep(als_ctx* c, int t) {
   const int sidx = 1 - t;
   Side& S = c->s[sidx];
@@ -1000,7 +1060,9 @@ int half_sweep(als_ctx* c, int t) {
     return fail(ALS_E_NOT_POSITIVE_DEFINITE,
                 "LAPACK.dppsv-equivalent Cholesky met a non-positive pivot because A is not positive "
                 "definite. Is A derived from a singular matrix (e.g. collinear column values)? (flags " +
-                    std::to_string(err) + err_paths(err) + ", " + std::to_string(sweeps) + " eigensolver sweeps)");
+                    std::to_string(err) + err_paths(err) + ", " + std::to_string(sweeps) + " eigensolver sweeps, " +
+                    (t == ALS_USER ? "user" : "item") + " half)" +
+                    failure_diag(c, S, T, c->p.implicit_prefs ? (multi ? S.prows() : S.own_n) : S.own_n, zhl));
   T.has_factors = true;
   T.orig_valid = false;
   T.full_valid = multi;  // gathered behind the solve (st2); the next half waits for it
@@ -1508,7 +1570,17 @@ struct TopkPlan {
   int64_t n_chunks = 0, n_super = 0;
   bool prune = false;
   DevBuf d_th, d_keys, d_perm, d_nperm, d_tp, d_tmp, d_dstids, d_VP, d_cfeat, d_supf, d_probe, d_slab, d_G;
-  DevBuf d_src, d_ls, d_lc, d_need, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp, d_thr, d_sf, d_mask, d_kth;
+  DevBuf d_src, d_ls, d_lc, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp, d_thr, d_sf, d_mask, d_kth;
+  // per call (topk_begin .. topk_finish): the passes run back to back with no host round trip; their
+  // event pairs, scan counters (d_scan[pass]) and rows per scan workgroup are read at the end
+  DevBuf d_cnt;  // int [4]: this pass's flagged count, the rescan work counter, the call's flagged total
+  std::vector<hipEvent_t> evs;  // 5 per pass: start, mask done, scan done, select done, rescans done
+  std::vector<int> pass_rpw;
+  int64_t n_passes = 0;
+  ~TopkPlan() {
+    for (hipEvent_t e : evs)
+      if (e) (void)hipEventDestroy(e);
+  }
 };
 
 // The leading TOPK_M eigenvectors of the dst side's Gram Σ t tᵀ (original basis), fp64 [TOPK_M][KP]:
@@ -1605,23 +1677,66 @@ int topk_plan(als_ctx* c, int src, int k, TopkPlan& P) {
   return ALS_OK;
 }
 
-// Top-k of the nc src rows `rows` (host, dense row indices) into the device lists d_oid / d_osc
-// ([nc][k], score desc, id asc); rows that fail certification are re-scored exactly and their ids
-// appended to c->last_rescan.  Enqueued on c->st; returns after the rescans are enqueued.
-int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int32_t* d_oid, float* d_osc) {
+// A call's top-k passes: topk_begin (n_rows positions, at most n_passes passes; the rescan flags of
+// position p land in c->d_last_need[p]), topk_run_rows per pass, topk_finish (one synchronisation:
+// timers and counters).
+int topk_begin(als_ctx* c, TopkPlan& P, int64_t n_rows, int64_t n_passes, const int32_t* rows) {
+  HIPCHK(P.d_scan.ensure((size_t)std::max<int64_t>(n_passes, 1) * 8));
+  HIPCHK(hipMemsetAsync(P.d_scan.p, 0, (size_t)std::max<int64_t>(n_passes, 1) * 8, c->st));
+  HIPCHK(P.d_cnt.ensure(16));
+  HIPCHK(hipMemsetAsync(P.d_cnt.p, 0, 16, c->st));
+  HIPCHK(c->d_last_need.ensure((size_t)std::max<int64_t>(n_rows, 1) * 4));
+  HIPCHK(hipMemsetAsync(c->d_last_need.p, 0, (size_t)std::max<int64_t>(n_rows, 1) * 4, c->st));
+  c->last_need_n = n_rows;
+  c->last_src = P.src;
+  c->last_rows_dense = rows == nullptr;
+  if (rows) c->last_rows.assign(rows, rows + n_rows);
+  else c->last_rows.clear();
+  c->last_rescan.clear();
+  c->last_rescan_ready = false;
+  P.n_passes = n_passes;
+  P.pass_rpw.clear();
+  return ALS_OK;
+}
+
+int topk_finish(als_ctx* c, TopkPlan& P) {
+  HIPCHK(hipStreamSynchronize(c->st));
+  const int64_t np = (int64_t)P.pass_rpw.size();
+  std::vector<unsigned long long> scanned((size_t)std::max<int64_t>(np, 1), 0ull);
+  int cnt[4] = {0, 0, 0, 0};
+  if (np > 0) HIPCHK(hipMemcpy(scanned.data(), P.d_scan.p, np * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(cnt, P.d_cnt.p, 16, hipMemcpyDeviceToHost));
+  for (int64_t q = 0; q < np; ++q) {
+    hipEvent_t* e = P.evs.data() + 5 * q;
+    c->topk_ms[0] += event_ms(e[0], e[1]);
+    c->topk_ms[1] += event_ms(e[1], e[2]);
+    c->topk_ms[2] += event_ms(e[2], e[3]);
+    c->topk_ms[3] += event_ms(e[3], e[4]);
+    c->topk_stats[2] += (int64_t)scanned[q];
+    c->topk_ms[4] += (double)scanned[q] * (P.pass_rpw[q] / 4) * 2.0 * c->KP;  // per wave: rpw / 4 src rows x each dst row
+  }
+  c->topk_stats[1] += cnt[2];
+  return ALS_OK;
+}
+
+// One pass: the nc src rows `rows` (host, dense row indices; nullptr: rows row0 .. row0 + nc - 1,
+// generated on the device) at positions pos0 .. pos0 + nc - 1 of the call, into the device lists
+// d_oid / d_osc ([nc][k], score desc, id asc).  Rows that fail certification are compacted on the
+// device and re-scored by a persistent exact scan in the same stream: nothing here waits for the GPU.
+int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t row0, int64_t pos0, int64_t nc, int32_t* d_oid,
+                  float* d_osc) {
   Side& S = c->s[P.src];
   Side& T = c->s[1 - P.src];
   const int KP = c->KP, k = P.k;
   if (nc <= 0) return ALS_OK;
   HIPCHK(P.d_src.ensure(nc * 4));
-  HIPCHK(P.d_need.ensure(nc * 4));
   if (!P.exact_only) {
     HIPCHK(P.d_ls.ensure(nc * TOPK_CAP * 8));
     HIPCHK(P.d_lc.ensure(nc * 4));
   }
-  HIPCHK(hipMemcpyAsync(P.d_src.p, rows, nc * 4, hipMemcpyHostToDevice, c->st));
-  HIPCHK(hipMemsetAsync(P.d_need.p, 0, nc * 4, c->st));
-  HIPCHK(hipMemsetAsync(P.d_scan.p, 0, 8, c->st));
+  if (rows) HIPCHK(hipMemcpyAsync(P.d_src.p, rows, nc * 4, hipMemcpyHostToDevice, c->st));
+  else HIPCHK(launch_iota_i32(P.d_src.as<int32_t>(), nc, row0, c->st));
+  (void)S;
   TopkArgs a{};
   a.S = S.d_orig.as<float>();
   a.T = T.d_orig.as<float>();
@@ -1647,20 +1762,29 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int3
   a.lcnt = P.d_lc.as<int32_t>();
   a.out_ids = d_oid;
   a.out_scores = d_osc;
-  a.need_exact = P.d_need.as<int32_t>();
+  int32_t* d_need = c->d_last_need.as<int32_t>() + pos0;
+  a.need_exact = d_need;
   if (!P.exact_only) {
     HIPCHK(P.d_kth.ensure(nc * 4));
     a.kth0 = P.d_kth.as<float>();
   }
-  a.scanned = P.d_scan.as<unsigned long long>();
+  const int64_t pass = (int64_t)P.pass_rpw.size();
+  if (pass >= P.n_passes) return fail(ALS_E_STATE, "top-k: more passes than planned");
+  a.scanned = P.d_scan.as<unsigned long long>() + pass;
   if (P.exact_only) {
     HIPCHK(launch_topk_exact(KP, a, nullptr, nc, c->st));
     return ALS_OK;
   }
+  while ((int64_t)P.evs.size() < 5 * (pass + 1)) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    P.evs.push_back(e);
+  }
+  hipEvent_t* ev = P.evs.data() + 5 * pass;
   // scan order: rows that stop at similar depths share a workgroup (topk_order); the select writes
   // each row's results back to its own slot
   TopkArgs b = a;
-  HIPCHK(hipEventRecord(c->evt[0], c->st));
+  HIPCHK(hipEventRecord(ev[0], c->st));
   HIPCHK(P.d_okeys.ensure(nc * 8));
   HIPCHK(P.d_order.ensure(nc * 8));
   HIPCHK(P.d_srcs.ensure(nc * 4));
@@ -1684,39 +1808,19 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t nc, int3
     b.mask = P.d_mask.as<uint32_t>();
     HIPCHK(launch_topk_mask(b, rpw, P.d_supf.as<float>(), P.n_super, P.d_mask.as<uint32_t>(), c->st));
   }
-  HIPCHK(hipEventRecord(c->evt[1], c->st));
+  HIPCHK(hipEventRecord(ev[1], c->st));
   HIPCHK(launch_topk(KP, b, c->n_cu, c->st));
-  HIPCHK(hipEventRecord(c->evt[2], c->st));
+  HIPCHK(hipEventRecord(ev[2], c->st));
   HIPCHK(launch_topk_select(KP, b, c->st));
-  HIPCHK(hipEventRecord(c->evt[3], c->st));
-  std::vector<int32_t> need(nc);
-  unsigned long long scanned = 0;
-  HIPCHK(hipMemcpyAsync(need.data(), P.d_need.p, nc * 4, hipMemcpyDeviceToHost, c->st));
-  HIPCHK(hipMemcpyAsync(&scanned, P.d_scan.p, 8, hipMemcpyDeviceToHost, c->st));
-  HIPCHK(hipStreamSynchronize(c->st));
-  std::vector<int32_t> flagged;
-  for (int64_t i = 0; i < nc; ++i)
-    if (need[i]) {
-      flagged.push_back((int32_t)i);
-      c->last_rescan.push_back(S.ids[rows[i]]);
-    }
+  HIPCHK(hipEventRecord(ev[3], c->st));
+  // certification failures: compacted on the device (pass-local positions), re-scored in place
+  HIPCHK(hipMemsetAsync(P.d_cnt.p, 0, 8, c->st));  // this pass's count and work counter
+  HIPCHK(P.d_flag.ensure(nc * 4));
+  HIPCHK(launch_topk_exact_flagged(KP, a, d_need, nc, P.d_flag.as<int32_t>(), P.d_cnt.as<int>(), c->n_cu, c->st));
+  HIPCHK(hipEventRecord(ev[4], c->st));
+  P.pass_rpw.push_back(rpw);
   c->topk_stats[0] += nc;
-  c->topk_stats[1] += (int64_t)flagged.size();
-  c->topk_stats[2] += (int64_t)scanned;
   c->topk_stats[3] += (nc + rpw - 1) / rpw * 4 * P.n_chunks * P.CH;  // dst rows x waves
-  c->topk_ms[0] += event_ms(c->evt[0], c->evt[1]);
-  c->topk_ms[1] += event_ms(c->evt[1], c->evt[2]);
-  c->topk_ms[2] += event_ms(c->evt[2], c->evt[3]);
-  c->topk_ms[4] += (double)scanned * (rpw / 4) * 2.0 * KP;  // per wave: rpw / 4 src rows x each dst row
-  if (!flagged.empty()) {
-    HIPCHK(P.d_flag.ensure(flagged.size() * 4));
-    HIPCHK(hipMemcpyAsync(P.d_flag.p, flagged.data(), flagged.size() * 4, hipMemcpyHostToDevice, c->st));
-    HIPCHK(hipEventRecord(c->evt[0], c->st));
-    HIPCHK(launch_topk_exact(KP, a, P.d_flag.as<int32_t>(), (int64_t)flagged.size(), c->st));
-    HIPCHK(hipEventRecord(c->evt[4], c->st));
-    HIPCHK(hipStreamSynchronize(c->st));  // flagged (host) must outlive the async copy
-    c->topk_ms[3] += event_ms(c->evt[0], c->evt[4]);
-  }
   return ALS_OK;
 }
 
@@ -1728,48 +1832,72 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   if (k > TOPK_MAX)
     return fail(ALS_E_UNSUPPORTED, "num above " + std::to_string(TOPK_MAX) + " is not supported by this engine");
   TRYC(set_device(c));
+  // ALBEDO_TOPK_TRACE (diagnostic): wall-clock stamps of the call's phases on stderr, the stream
+  // synchronised at each (so the stamps bracket device work)
+  static const bool trace = [] {
+    const char* e = std::getenv("ALBEDO_TOPK_TRACE");
+    return e && *e && *e != '0';
+  }();
+  const auto t_start = std::chrono::steady_clock::now();
+  auto stamp = [&](const char* what) {
+    if (!trace) return;
+    (void)hipStreamSynchronize(c->st);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    std::fprintf(stderr, "[topk] %9.2f ms  %s\n", ms, what);
+  };
   const int src = side;
   TRYC(materialize(c, src));
+  stamp("materialize src");
   Side& S = c->s[src];
   const Side& T = c->s[1 - src];
   const int64_t nq = subset ? n_subset : S.n;
-  // id -> row: a merge walk when the subset is ascending (the usual case), binary search otherwise
-  std::vector<int32_t> qrow(nq);
-  if (!subset) {
-    for (int64_t i = 0; i < nq; ++i) qrow[i] = (int32_t)i;
-  } else if (std::is_sorted(subset, subset + nq)) {
-    int64_t r = 0;
-    for (int64_t i = 0; i < nq; ++i) {
-      while (r < S.n && S.ids[r] < subset[i]) ++r;
-      qrow[i] = (r < S.n && S.ids[r] == subset[i]) ? (int32_t)r : -1;
-    }
-  } else {
-    for (int64_t i = 0; i < nq; ++i) qrow[i] = (int32_t)find_row(S, subset[i]);
-  }
-  if (src_ids_out)
-    for (int64_t i = 0; i < nq; ++i) src_ids_out[i] = subset ? subset[i] : S.ids[i];
+  // recommendForAll*: every src row, in row order -- no host index arrays (the device generates the
+  // row indices of each pass); a subset: id -> row by a merge walk when ascending (the usual case),
+  // binary search otherwise, unknown ids padded here
+  const bool all_rows = subset == nullptr;
   std::vector<int32_t> known;
   std::vector<int64_t> pos;
-  known.reserve(nq);
-  pos.reserve(nq);
-  for (int64_t i = 0; i < nq; ++i)
-    if (qrow[i] >= 0) {
-      known.push_back(qrow[i]);
-      pos.push_back(i);
+  if (!all_rows) {
+    std::vector<int32_t> qrow(nq);
+    if (std::is_sorted(subset, subset + nq)) {
+      int64_t r = 0;
+      for (int64_t i = 0; i < nq; ++i) {
+        while (r < S.n && S.ids[r] < subset[i]) ++r;
+        qrow[i] = (r < S.n && S.ids[r] == subset[i]) ? (int32_t)r : -1;
+      }
     } else {
-      std::fill(dst_ids_out + i * k, dst_ids_out + (i + 1) * k, -1);
-      std::fill(scores_out + i * k, scores_out + (i + 1) * k, NAN);
+      for (int64_t i = 0; i < nq; ++i) qrow[i] = (int32_t)find_row(S, subset[i]);
     }
-  const bool dense_out = (int64_t)known.size() == nq;  // results land in place, no scatter
+    known.reserve(nq);
+    pos.reserve(nq);
+    for (int64_t i = 0; i < nq; ++i)
+      if (qrow[i] >= 0) {
+        known.push_back(qrow[i]);
+        pos.push_back(i);
+      } else {
+        std::fill(dst_ids_out + i * k, dst_ids_out + (i + 1) * k, -1);
+        std::fill(scores_out + i * k, scores_out + (i + 1) * k, NAN);
+      }
+  }
+  if (src_ids_out) {
+    if (all_rows) std::memcpy(src_ids_out, S.ids.data(), (size_t)nq * 4);
+    else std::memcpy(src_ids_out, subset, (size_t)nq * 4);
+  }
+  const int64_t n_known = all_rows ? nq : (int64_t)known.size();
+  auto posf = [&](int64_t i) { return all_rows ? i : pos[i]; };           // output slot of known row i
+  auto rowsf = [&](int64_t q0) { return all_rows ? nullptr : known.data() + q0; };  // null: rows q0 ..
+  const bool dense_out = n_known == nq;  // results land in place, no scatter
   c->last_rescan.clear();
-  if (known.empty() || T.n == 0) return ALS_OK;
+  c->last_rescan_ready = true;
+  if (n_known == 0 || T.n == 0) return ALS_OK;
+  stamp("host id mapping");
   TopkPlan P;
   TRYC(topk_plan(c, src, k, P));
+  stamp("plan (materialize dst, Gram + host eig, dst sort + fp16 pack)");
   // 4M src rows per pass (candidate lists 4 GB): fewer launch tails than 1M-row passes
   const int64_t chunk = 1 << 22;
   // world > 1 (SURVEY §8(e) "Top-k: shard users"): rank r scores the r-th contiguous slice of the
   // known src rows against the replicated dst factors; the lists are all-gathered afterwards
-  const int64_t n_known = (int64_t)known.size();
   const int64_t per_rank = (n_known + c->world - 1) / c->world;
   const int64_t lo = std::min<int64_t>(n_known, (int64_t)c->rank * per_rank);
   const int64_t hi = std::min<int64_t>(n_known, lo + per_rank);
@@ -1787,6 +1915,7 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
       else (void)hipHostUnregister(dst_ids_out + lo * k);
     }
     (void)hipGetLastError();  // a refused registration is not an error: the synchronous path runs
+    stamp("pin the output arrays");
   }
   // releases everything the async path holds (null-safe: also after a partial set-up)
   auto end_async = [&]() {
@@ -1818,6 +1947,13 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
     }
   }
   DevBuf d_oid, d_osc;
+  {
+    const int rc = topk_begin(c, P, n_known, (hi - lo + chunk - 1) / chunk, all_rows ? nullptr : known.data());
+    if (rc != ALS_OK) {
+      end_async();
+      return rc;
+    }
+  }
   for (int64_t q0 = lo, it = 0; q0 < hi; q0 += chunk, ++it) {
     const int64_t nc = std::min<int64_t>(chunk, hi - q0);
     if (async_out) {
@@ -1826,7 +1962,7 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
       if (it >= 2 && hipStreamWaitEvent(c->st, ev_copy[b], 0) != hipSuccess) rc = fail(ALS_E_HIP, "stream wait");
       if (rc == ALS_OK && (d_oid2[b].ensure(nc * k * 4) != hipSuccess || d_osc2[b].ensure(nc * k * 4) != hipSuccess))
         rc = fail(ALS_E_OUT_OF_MEMORY, "top-k output buffers");
-      if (rc == ALS_OK) rc = topk_run_rows(c, P, known.data() + q0, nc, d_oid2[b].as<int32_t>(), d_osc2[b].as<float>());
+      if (rc == ALS_OK) rc = topk_run_rows(c, P, rowsf(q0), q0, q0, nc, d_oid2[b].as<int32_t>(), d_osc2[b].as<float>());
       if (rc == ALS_OK &&
           (hipEventRecord(ev_comp[b], c->st) != hipSuccess || hipStreamWaitEvent(cs, ev_comp[b], 0) != hipSuccess ||
            hipMemcpyAsync(dst_ids_out + q0 * k, d_oid2[b].p, nc * k * 4, hipMemcpyDeviceToHost, cs) != hipSuccess ||
@@ -1837,11 +1973,12 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
         end_async();
         return rc;
       }
+      stamp("pass");
       continue;
     }
     HIPCHK(d_oid.ensure(nc * k * 4));
     HIPCHK(d_osc.ensure(nc * k * 4));
-    TRYC(topk_run_rows(c, P, known.data() + q0, nc, d_oid.as<int32_t>(), d_osc.as<float>()));
+    TRYC(topk_run_rows(c, P, rowsf(q0), q0, q0, nc, d_oid.as<int32_t>(), d_osc.as<float>()));
     if (dense_out) {
       HIPCHK(hipMemcpyAsync(dst_ids_out + q0 * k, d_oid.p, nc * k * 4, hipMemcpyDeviceToHost, c->st));
       HIPCHK(hipMemcpyAsync(scores_out + q0 * k, d_osc.p, nc * k * 4, hipMemcpyDeviceToHost, c->st));
@@ -1853,18 +1990,26 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
       HIPCHK(hipMemcpyAsync(osc.data(), d_osc.p, osc.size() * 4, hipMemcpyDeviceToHost, c->st));
       HIPCHK(hipStreamSynchronize(c->st));
       for (int64_t i = 0; i < nc; ++i) {
-        std::memcpy(dst_ids_out + pos[q0 + i] * k, &oid[i * k], k * 4);
-        std::memcpy(scores_out + pos[q0 + i] * k, &osc[i * k], k * 4);
+        std::memcpy(dst_ids_out + posf(q0 + i) * k, &oid[i * k], k * 4);
+        std::memcpy(scores_out + posf(q0 + i) * k, &osc[i * k], k * 4);
       }
     }
   }
+  {
+    const int rc = topk_finish(c, P);
+    if (rc != ALS_OK) {
+      end_async();
+      return rc;
+    }
+  }
   end_async();
+  stamp("last copies + unpin");
   if (c->world > 1 && per_rank > 0) {  // every rank ends with every list: one all-gather of the slices
     std::vector<float> blk((size_t)c->world * per_rank * k * 2, 0.f);
     float* mine = blk.data() + (size_t)c->rank * per_rank * k * 2;
     for (int64_t i = lo; i < hi; ++i) {
-      std::memcpy(mine + (size_t)(i - lo) * k * 2, dst_ids_out + pos[i] * k, k * 4);
-      std::memcpy(mine + (size_t)(i - lo) * k * 2 + k, scores_out + pos[i] * k, k * 4);
+      std::memcpy(mine + (size_t)(i - lo) * k * 2, dst_ids_out + posf(i) * k, k * 4);
+      std::memcpy(mine + (size_t)(i - lo) * k * 2 + k, scores_out + posf(i) * k, k * 4);
     }
     TRYC(allgather_host(c, blk.data(), per_rank * k * 2));
     for (int r = 0; r < c->world; ++r) {
@@ -1872,8 +2017,8 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
       const int64_t rl = std::min<int64_t>(n_known, (int64_t)r * per_rank), rh = std::min<int64_t>(n_known, rl + per_rank);
       const float* bb = blk.data() + (size_t)r * per_rank * k * 2;
       for (int64_t i = rl; i < rh; ++i) {
-        std::memcpy(dst_ids_out + pos[i] * k, bb + (size_t)(i - rl) * k * 2, k * 4);
-        std::memcpy(scores_out + pos[i] * k, bb + (size_t)(i - rl) * k * 2 + k, k * 4);
+        std::memcpy(dst_ids_out + posf(i) * k, bb + (size_t)(i - rl) * k * 2, k * 4);
+        std::memcpy(scores_out + posf(i) * k, bb + (size_t)(i - rl) * k * 2 + k, k * 4);
       }
     }
   }
@@ -1892,6 +2037,7 @@ int als_evaluate_ndcg(als_ctx* c, int32_t k, int64_t n, const int32_t* user, con
   *ndcg_out = NAN;
   *n_users_out = 0;
   c->last_rescan.clear();
+  c->last_rescan_ready = true;
   if (n <= 0 || S.n == 0) return ALS_OK;
   hipStream_t st = c->st;
   // 1. intoUserActualItems on the device: group by model user (inner join), top-k by (key desc, item asc)
@@ -1940,14 +2086,16 @@ int als_evaluate_ndcg(als_ctx* c, int32_t k, int64_t n, const int32_t* user, con
   const int64_t lo = std::min<int64_t>(nr, (int64_t)c->rank * per_rank), hi = std::min<int64_t>(nr, lo + per_rank);
   const int64_t chunk = 1 << 20;
   DevBuf d_oid, d_osc;
+  TRYC(topk_begin(c, P, nr, (hi - lo + chunk - 1) / chunk, rows.data()));
   for (int64_t q0 = lo; q0 < hi; q0 += chunk) {
     const int64_t nc = std::min<int64_t>(chunk, hi - q0);
     HIPCHK(d_oid.ensure(nc * k * 4));
     HIPCHK(d_osc.ensure(nc * k * 4));
-    TRYC(topk_run_rows(c, P, rows.data() + q0, nc, d_oid.as<int32_t>(), d_osc.as<float>()));
+    TRYC(topk_run_rows(c, P, rows.data() + q0, 0, q0, nc, d_oid.as<int32_t>(), d_osc.as<float>()));
     HIPCHK(eval_ndcg(d_oid.as<int32_t>(), d_act.as<int32_t>() + q0 * k, d_actn.as<int32_t>() + q0, nc, k,
                      d_gain.as<double>(), d_vals.as<double>() + q0, st));
   }
+  TRYC(topk_finish(c, P));
   std::vector<double> vals((size_t)std::max<int64_t>(per_rank, 1) * c->world, 0.0);
   if (hi > lo)
     HIPCHK(hipMemcpyAsync(vals.data() + (size_t)c->rank * per_rank, d_vals.as<double>() + lo, (hi - lo) * 8,
@@ -2060,6 +2208,19 @@ int als_topk_timing(const als_ctx* c, double* out5) {
 
 int als_topk_last_rescan(const als_ctx* c, int32_t* src_ids_out, int64_t cap, int64_t* n_out) {
   if (!c || !n_out) return fail(ALS_E_INVALID_ARGUMENT, "bad args");
+  if (!c->last_rescan_ready) {  // first query after a top-k call: read its device flags
+    TRYC(set_device(const_cast<als_ctx*>(c)));
+    std::vector<int32_t> need((size_t)c->last_need_n);
+    if (c->last_need_n > 0) {
+      HIPCHK(hipStreamSynchronize(c->st));
+      HIPCHK(hipMemcpy(need.data(), c->d_last_need.p, need.size() * 4, hipMemcpyDeviceToHost));
+    }
+    const Side& S = c->s[c->last_src];
+    c->last_rescan.clear();
+    for (int64_t p = 0; p < c->last_need_n; ++p)
+      if (need[p]) c->last_rescan.push_back(S.ids[c->last_rows_dense ? p : c->last_rows[p]]);
+    c->last_rescan_ready = true;
+  }
   *n_out = (int64_t)c->last_rescan.size();
   if (src_ids_out && *n_out <= cap) std::memcpy(src_ids_out, c->last_rescan.data(), c->last_rescan.size() * 4);
   return ALS_OK;

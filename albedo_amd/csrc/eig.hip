@@ -389,6 +389,32 @@ const int* eig_sweeps(const double* scratch, int KP) {
   return reinterpret_cast<const int*>(scratch + (size_t)3 * KP * KP + KP + 2);
 }
 
+__global__ void diag_scan_kernel(const void* __restrict__ p, int64_t n, bool f16, unsigned long long* __restrict__ out) {
+  unsigned long long bad = 0, first = ~0ull;
+  unsigned mx = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = f16 ? (float)reinterpret_cast<const _Float16*>(p)[i] : reinterpret_cast<const float*>(p)[i];
+    if (!isfinite(v)) {
+      ++bad;
+      if ((unsigned long long)i < first) first = (unsigned long long)i;
+    } else {
+      mx = max(mx, __float_as_uint(fabsf(v)));
+    }
+  }
+  if (bad) {
+    atomicAdd(out, bad);
+    atomicMin(out + 1, first);
+  }
+  if (mx) atomicMax(out + 2, (unsigned long long)mx);
+}
+
+hipError_t launch_diag_scan(const void* p, int64_t n, bool f16, unsigned long long* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  diag_scan_kernel<<<(int)blocks, 256, 0, s>>>(p, n, f16, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_identity(double* B, int KP, hipStream_t s) {
   identity_kernel<<<(KP * KP + 255) / 256, 256, 0, s>>>(B, KP);
   return hipGetLastError();

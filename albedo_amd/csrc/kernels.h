@@ -200,6 +200,12 @@ hipError_t launch_topk_mask(const TopkArgs& a, int rows_per_wg, const float* sup
 int topk_rows_per_workgroup(int KP, int64_t n_src, int n_cu);
 // exact full scan for the given src-row indices (rows == null: rows 0 .. n_rows-1), any k <= TOPK_MAX
 hipError_t launch_topk_exact(int KP, const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s);
+hipError_t launch_iota_i32(int32_t* out, int64_t n, int64_t start, hipStream_t s);  // out[i] = start + i
+// the certification rescans without a host round trip: need[0 .. n) compacted into flags (cnt[0]: their
+// count, cnt[1]: the persistent grid's work counter, both zero on entry; cnt[2] += the count), then a
+// persistent exact scan over them
+hipError_t launch_topk_exact_flagged(int KP, const TopkArgs& a, const int32_t* need, int64_t n, int32_t* flags, int* cnt,
+                                     int n_cu, hipStream_t s);
 // ---- evaluation (eval.hip): RankingEvaluator.scala:83-139 on the device ----------------------------
 size_t eval_sort_temp_bytes(int64_t n);
 // user ids -> rows of the ascending `ids`, grouped: runs[r] (row) with counts[r] entries at
@@ -234,6 +240,10 @@ struct ShardStarts {
 // (l / chpad)·world·chpad + r·chpad + l % chpad (chunk-major: one chunk of every rank is contiguous)
 hipError_t padded_remap(const int32_t* d_in, int64_t n, const ShardStarts& st, int64_t chpad, int32_t* d_out,
                         hipStream_t s);
+// Failure diagnostics (not on the hot path): over n values of p (fp32, or fp16 when f16),
+// out[0] += non-finite count, out[1] = min index of a non-finite value (atomicMin; caller sets it to
+// ~0), out[2] = max |finite value| as float bits (atomicMax; caller zeroes it)
+hipError_t launch_diag_scan(const void* p, int64_t n, bool f16, unsigned long long* out, hipStream_t s);
 // Synthetic generator (synth.hip)
 hipError_t synth_fill(uint64_t seed, int rounds, int64_t n_users, int64_t n_items,
                       const int64_t* d_deg_prefix, const double* d_cw, const int32_t* d_perm,

@@ -409,32 +409,48 @@ __global__ __launch_bounds__(256, (TkScan<KP, G>::OCC)) void topk_scan_kernel(To
     TKPH_N(4, __popcll(f0) + __popcll(f1));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's list stores are in L2
     TKPH(6);  // the drain of every outstanding VMEM op (ring DMAs included) before a compaction
+    // two rows per batch: the list loads of both are in flight together (a compaction event flags
+    // ~1.8 rows at c4); no drain after the batch (appends go to positions >= 64, and the next
+    // compaction drains before it reads)
     while (f0 | f1) {
-      int wl;
-      if (f0) { wl = __builtin_ctzll(f0); f0 &= f0 - 1; }
-      else { wl = 64 + __builtin_ctzll(f1); f1 &= f1 - 1; }
-      uint32_t cw = 0;  // the row's length: byte (wl & 3) of cntp[wl >> 4] in lane 16·((wl >> 2) & 3)
+      int wl[2];
+      bool on[2];
 #pragma unroll
-      for (int gi = 0; gi < G; ++gi)
-        if ((wl >> 4) == gi) cw = (uint32_t)rdlane_i((int)cntp[gi], 16 * ((wl >> 2) & 3));
-      const int cnt = (int)((cw >> (8 * (wl & 3))) & 0xffu);
-      const int64_t lb = (rb0 + wr0 + wl) * CAP;
-      float s2[NSC];
-      int i2[NSC];
-#pragma unroll
-      for (int h = 0; h < NSC; ++h) {
-        const int e = lane + 64 * h;
-        const uint64_t v = e < cnt ? agent_load64(reinterpret_cast<const uint64_t*>(a.lent + lb + e))
-                                   : ((uint64_t)0xFFFFFFFFu << 32) | __float_as_uint(-INFINITY);
-        s2[h] = __uint_as_float((uint32_t)v);
-        i2[h] = (int)(uint32_t)(v >> 32);
+      for (int k = 0; k < 2; ++k) {
+        on[k] = (f0 | f1) != 0;
+        wl[k] = 0;
+        if (f0) { wl[k] = __builtin_ctzll(f0); f0 &= f0 - 1; }
+        else if (f1) { wl[k] = 64 + __builtin_ctzll(f1); f1 &= f1 - 1; }
       }
-      wave_bitonic<NSC>(s2, i2);
-      a.lent[lb + lane] = uint2{__float_as_uint(s2[0]), (uint32_t)i2[0]};
-      const float tkt = rdlane(s2[0], a.kt - 1);  // the running kt-th best becomes the threshold
-      if (lane == 0) s_thr[wr0 + wl] = tkt;
+      float s2[2][NSC];
+      int i2[2][NSC];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        uint32_t cw = 0;  // the row's length: byte (wl & 3) of cntp[wl >> 4] in lane 16·((wl >> 2) & 3)
+#pragma unroll
+        for (int gi = 0; gi < G; ++gi)
+          if ((wl[k] >> 4) == gi) cw = (uint32_t)rdlane_i((int)cntp[gi], 16 * ((wl[k] >> 2) & 3));
+        const int cnt = on[k] ? (int)((cw >> (8 * (wl[k] & 3))) & 0xffu) : 0;
+        const int64_t lb = (rb0 + wr0 + wl[k]) * CAP;
+#pragma unroll
+        for (int h = 0; h < NSC; ++h) {
+          const int e = lane + 64 * h;
+          const uint64_t v = e < cnt ? agent_load64(reinterpret_cast<const uint64_t*>(a.lent + lb + e))
+                                     : ((uint64_t)0xFFFFFFFFu << 32) | __float_as_uint(-INFINITY);
+          s2[k][h] = __uint_as_float((uint32_t)v);
+          i2[k][h] = (int)(uint32_t)(v >> 32);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (!on[k]) continue;  // wave-uniform
+        wave_bitonic<NSC>(s2[k], i2[k]);
+        const int64_t lb = (rb0 + wr0 + wl[k]) * CAP;
+        a.lent[lb + lane] = uint2{__float_as_uint(s2[k][0]), (uint32_t)i2[k][0]};
+        const float tkt = rdlane(s2[k][0], a.kt - 1);  // the running kt-th best becomes the threshold
+        if (lane == 0) s_thr[wr0 + wl[k]] = tkt;
+      }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     WAVE_LDS_SYNC();
 #pragma unroll
     for (int gi = 0; gi < G; ++gi)
@@ -848,12 +864,28 @@ __global__ __launch_bounds__(256) void topk_mask_kernel(TopkArgs a, int rwg, con
 // best is skipped: none of its rows can enter the merged top-k (<= 64·P), ties included.  The bounds
 // are evaluated 64 chunks at a time (a lane per chunk), so a pruned chunk costs a fraction of one
 // feature-load latency instead of a dependent load per 64 rows.
+// dcount != null (the certification rescans, r05): a persistent grid takes the rows rows[0 ..
+// *dcount) from the counter *dnext, so the host never waits for the flagged count.
 template <int KP, int P>
-__global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32_t* rows, int64_t row0) {
+__global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32_t* rows, int64_t row0,
+                                                         const int* dcount, int* dnext) {
   __shared__ float msc[4][64 * P];
   __shared__ int mix[4][64 * P];
+  __shared__ int s_idx;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t si = rows ? rows[row0 + blockIdx.x] : row0 + (int64_t)blockIdx.x;
+  for (int64_t it = 0;; ++it) {
+  int64_t si;
+  if (dcount) {
+    if (threadIdx.x == 0) s_idx = atomicAdd(dnext, 1);
+    __syncthreads();
+    const int idx = s_idx;
+    __syncthreads();  // s_idx read by every thread before the next claim rewrites it
+    if (idx >= *dcount) return;  // workgroup-uniform
+    si = rows[idx];
+  } else {
+    if (it > 0) return;
+    si = rows ? rows[row0 + blockIdx.x] : row0 + (int64_t)blockIdx.x;
+  }
   const int srow = a.src_rows[si];
   const float* s = a.S + (int64_t)srow * KP;
   float bs[2 * P];
@@ -953,6 +985,8 @@ __global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32
         a.out_scores[si * a.k + e] = idx >= 0 ? bs[h] : __int_as_float(0x7fc00000);
       }
     }
+  }
+  __syncthreads();  // msc / mix read by wave 0 before the next row's waves rewrite them
   }
 }
 
@@ -1131,13 +1165,13 @@ hipError_t launch_scan(const TopkArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// src rows per scan workgroup: the largest register blocking (G = 8 at KP <= 128, 4 at KP = 256)
-// that still gives every CU two workgroups, down to G = 2
+// src rows per scan workgroup: register blocking G = 4 (two workgroups per CU: r05, c4 all users
+// scan 649 -> 438 ms against G = 8 at one per CU), smaller while it leaves CUs without two workgroups
 int topk_rows_per_workgroup(int KP, int64_t n_src, int n_cu) {
   int gmax = KP <= 128 ? 8 : 4;
   static const int gcap = [] {  // ALBEDO_TOPK_GMAX: A/B knob (2, 4 or 8)
     const char* e = std::getenv("ALBEDO_TOPK_GMAX");
-    return e && *e ? std::atoi(e) : 8;
+    return e && *e ? std::atoi(e) : 4;
   }();
   gmax = std::min(gmax, std::max(2, gcap));
   for (int G = gmax; G > 2; G /= 2)
@@ -1211,11 +1245,16 @@ template <int KP, int P>
 hipError_t topk_exact_p(const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s) {
   for (int64_t r0 = 0; r0 < n_rows; r0 += max_rows_per_launch(256)) {
     const int64_t n = std::min<int64_t>(n_rows - r0, max_rows_per_launch(256));
-    topk_exact_kernel<KP, P><<<(int)n, 256, 0, s>>>(a, rows, r0);
+    topk_exact_kernel<KP, P><<<(int)n, 256, 0, s>>>(a, rows, r0, nullptr, nullptr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+template <int KP, int P>
+hipError_t topk_exact_dev_p(const TopkArgs& a, const int32_t* rows, const int* dcount, int* dnext, int grid, hipStream_t s) {
+  topk_exact_kernel<KP, P><<<grid, 256, 0, s>>>(a, rows, 0, dcount, dnext);
+  return hipGetLastError();
 }
 template <int KP>
 hipError_t topk_exact_kp(const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s) {
@@ -1225,6 +1264,42 @@ hipError_t topk_exact_kp(const TopkArgs& a, const int32_t* rows, int64_t n_rows,
   if (a.k <= TOPK_MAX) return topk_exact_p<KP, 8>(a, rows, n_rows, s);
   return hipErrorInvalidValue;
 }
+// need[i] != 0 -> flags[atomicAdd(cnt, 1)] = i (order irrelevant: the rescan writes each row's own
+// slot); cnt[2] accumulates the call's total
+__global__ void topk_flag_compact_kernel(const int32_t* __restrict__ need, int64_t n, int32_t* __restrict__ flags,
+                                         int* __restrict__ cnt) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (need[i]) {
+      flags[atomicAdd(cnt, 1)] = (int32_t)i;
+      atomicAdd(cnt + 2, 1);
+    }
+}
+hipError_t launch_topk_exact_flagged(int KP, const TopkArgs& a, const int32_t* need, int64_t n, int32_t* flags, int* cnt,
+                                     int n_cu, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  topk_flag_compact_kernel<<<tk_grid(n, 256), 256, 0, s>>>(need, n, flags, cnt);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int grid = (int)std::min<int64_t>(n, (int64_t)4 * n_cu);
+  const int* dcount = cnt;
+  int* dnext = cnt + 1;
+  if (a.k > 64) return hipErrorInvalidValue;  // the certification path is k <= TOPK_KC
+  if (KP == 64) return topk_exact_dev_p<64, 1>(a, flags, dcount, dnext, grid, s);
+  if (KP == 128) return topk_exact_dev_p<128, 1>(a, flags, dcount, dnext, grid, s);
+  if (KP == 256) return topk_exact_dev_p<256, 1>(a, flags, dcount, dnext, grid, s);
+  return hipErrorInvalidValue;
+}
+
+__global__ void iota_i32_kernel(int32_t* __restrict__ out, int64_t n, int64_t start) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (int32_t)(start + i);
+}
+hipError_t launch_iota_i32(int32_t* out, int64_t n, int64_t start, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  iota_i32_kernel<<<tk_grid(n, 256), 256, 0, s>>>(out, n, start);
+  return hipGetLastError();
+}
+
 hipError_t launch_topk_exact(int KP, const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s) {
   if (n_rows <= 0) return hipSuccess;
   if (KP == 64) return topk_exact_kp<64>(a, rows, n_rows, s);

@@ -41,6 +41,7 @@ for s in "$@"; do
     pmc_topk4) timeout -k 10 600 tools/pmc_topk4.sh r04 > gpurun_out/pmc_topk4.log 2>&1 ;;
     bench_topk_g4) ALBEDO_TOPK_GMAX=4 timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk_g4.json 2> gpurun_out/bench_topk_g4.err ;;
     topkph_g4) ALBEDO_TOPK_GMAX=4 timeout -k 10 400 python -u tools/topk_phases.py --lib tools/ab/topkph.so --out gpurun_out/topkph_g4.json > gpurun_out/topkph_g4.log 2>&1 ;;
+    bench_topk_tr) ALBEDO_TOPK_TRACE=1 timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk_tr.json 2> gpurun_out/bench_topk_tr.err ;;
     bench_topk) timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk.json 2> gpurun_out/bench_topk.err ;;
     bench_c4q) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 > gpurun_out/bench_c4q.json 2> gpurun_out/bench_c4q.err ;;
     bench_c4q_l*) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 --light ${s#bench_c4q_l} > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
