@@ -546,10 +546,58 @@ __global__ __launch_bounds__(256, (TkScan<KP, G>::OCC)) void topk_scan_kernel(To
   if (a.scanned && lane == 0) atomicAdd(a.scanned, (unsigned long long)(n_scored * C::CH));
 }
 
+// F2J dots of a wave's candidate rows: lane L gets F2J(s, T[row_L]) (row_L < 0: -inf).  The rows
+// arrive in 32-column blocks, eight lanes per row (128 coalesced bytes per row instead of one 16-B
+// piece per lane and instruction), through the wave's LDS stage [64 rows][36 floats] (row stride 36:
+// the b128 reads of 16 consecutive rows hit 16 distinct bank groups); each lane then walks its own row
+// in F2J order (product, then add, left to right: f2j_dot_v4's value).
+constexpr int TK_SEL_LD = 36;
+template <int KP>
+__device__ __forceinline__ float f2j_dot_rows(const float* __restrict__ s, const float* __restrict__ T, int row, int kreal,
+                                              float* stg) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63, u = lane & 7;
+  float* sv = stg + 64 * TK_SEL_LD;  // the src row
+  for (int c = lane; c < KP; c += 64) sv[c] = s[c];
+  int rowm[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) rowm[m] = __shfl(row, (lane >> 3) + 8 * m);
+  float acc = 0.f;
+  const float* tr = stg + lane * TK_SEL_LD;
+  for (int cb = 0; cb < kreal; cb += 32) {
+    f32x4 v[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) v[m] = rowm[m] >= 0 ? ld4(T + (int64_t)rowm[m] * KP + cb + 4 * u) : zero4();
+    WAVE_LDS_SYNC();  // the previous block's reads are done
+#pragma unroll
+    for (int m = 0; m < 8; ++m) *reinterpret_cast<f32x4*>(stg + ((lane >> 3) + 8 * m) * TK_SEL_LD + 4 * u) = v[m];
+    WAVE_LDS_SYNC();
+    const int ce = kreal - cb < 32 ? kreal - cb : 32;
+    if (ce == 32) {
+#pragma unroll
+      for (int c = 0; c < 32; c += 4) {
+        const f32x4 t4 = ld4(tr + c), s4 = ld4(sv + cb + c);
+        const float p0 = s4[0] * t4[0], p1 = s4[1] * t4[1], p2 = s4[2] * t4[2], p3 = s4[3] * t4[3];
+        acc = acc + p0;
+        acc = acc + p1;
+        acc = acc + p2;
+        acc = acc + p3;
+      }
+    } else {
+      for (int c = 0; c < ce; ++c) {
+        const float p = sv[cb + c] * tr[c];
+        acc = acc + p;
+      }
+    }
+  }
+  return row >= 0 ? acc : -INFINITY;
+}
+
 // One wave per src row: best 64 of the list, exact F2J rescoring, sort, certify, write top-k.
 template <int KP>
 __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
   constexpr int CAP = TOPK_CAP, NS = CAP / 64;
+  __shared__ __attribute__((aligned(16))) float s_stage[4][64 * TK_SEL_LD + KP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t si = (int64_t)blockIdx.x * 4 + wave;
   if (si >= a.n_src) return;
@@ -575,8 +623,7 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
   // lower bound of the true k-th).  (Each rescored candidate reads a 512-B fp32 row from HBM.)
   const bool rescore = a.n_dst <= TOPK_KC || lane < a.kt;
   const int row = (i2[0] >= 0 && rescore) ? a.perm[i2[0]] : -1;
-  float ex = -INFINITY;
-  if (row >= 0) ex = f2j_dot_v4(s, a.T + (int64_t)row * KP, a.kreal);
+  const float ex = f2j_dot_rows<KP>(s, a.T, row, a.kreal, s_stage[wave]);
   double nn = 0.0;
   for (int c = lane; c < a.kreal; c += 64) nn += (double)s[c] * (double)s[c];
   for (int o = 32; o > 0; o >>= 1) nn += __shfl_xor(nn, o);

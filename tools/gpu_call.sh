@@ -23,6 +23,12 @@ for s in "$@"; do
     prof_c4) timeout -k 10 1100 tools/prof.sh c4 r03 16384 > gpurun_out/prof_c4.log 2>&1 ;;
     prof_c4r4) timeout -k 10 1100 tools/prof.sh c4 r04 16384 > gpurun_out/prof_c4r4.log 2>&1 ;;
     prof_c5r4) timeout -k 10 900 tools/prof.sh c5 r04 0 > gpurun_out/prof_c5r4.log 2>&1 ;;
+    prof_c4r5) timeout -k 10 1100 tools/prof.sh c4 r05 0 > gpurun_out/prof_c4r5.log 2>&1 ;;
+    prof_c5r5) timeout -k 10 900 tools/prof.sh c5 r05 0 > gpurun_out/prof_c5r5.log 2>&1 ;;
+    pmc_topk5) timeout -k 10 600 tools/pmc_topk4.sh r05 > gpurun_out/pmc_topk5.log 2>&1 ;;
+    multi) # back-to-back processes on one box (each a fresh context on memory the previous one freed)
+      for i in 1 2 3 4 5 6; do timeout -k 10 200 python -u bench.py --steps 2 --warmup 40 --no-cpu --topk-users 0 > gpurun_out/multi_$i.json 2> gpurun_out/multi_$i.err || { echo "multi run $i failed"; exit 1; }; done ;;
+    stress) timeout -k 10 300 python -u bench.py --steps 5 --warmup 300 --no-cpu --topk-users 0 > gpurun_out/stress.json 2> gpurun_out/stress.err ;;
     prof_c5) timeout -k 10 900 tools/prof.sh c5 r03 0 > gpurun_out/prof_c5.log 2>&1 ;;
     prof_c2) timeout -k 10 600 tools/prof.sh c2 r03 16384 > gpurun_out/prof_c2.log 2>&1 ;;
     trace_c4) mkdir -p gpurun_out/trace_c4 && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_c4 -o run -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu --topk-users 16384 > gpurun_out/trace_c4/bench.json 2> gpurun_out/trace_c4/bench.err ;;
