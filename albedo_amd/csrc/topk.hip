@@ -918,6 +918,7 @@ __global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32
                                                          const int* dcount, int* dnext) {
   __shared__ float msc[4][64 * P];
   __shared__ int mix[4][64 * P];
+  __shared__ __attribute__((aligned(16))) float s_stage[4][64 * TK_SEL_LD + KP];  // f2j_dot_rows
   __shared__ int s_idx;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int64_t it = 0;; ++it) {
@@ -972,7 +973,7 @@ __global__ __launch_bounds__(256) void topk_exact_kernel(TopkArgs a, const int32
   // 64 dst rows (one per lane) -> F2J scores, buffered when one of them reaches the threshold
   auto score64 = [&](int64_t pj, bool in) {
     const int64_t dj = (a.perm && in) ? (int64_t)a.perm[pj] : pj;
-    const float sc = in ? f2j_dot_v4(s, a.T + dj * KP, a.kreal) : -INFINITY;
+    const float sc = f2j_dot_rows<KP>(s, a.T, in ? (int)dj : -1, a.kreal, s_stage[wave]);
     if (!__any(sc >= thr)) return;
     static_for<0, P>([&](auto hh) {
       constexpr int h = decltype(hh)::value;
