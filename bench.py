@@ -207,14 +207,20 @@ def main():
     # Gram / rotation matrix-core evidence: MFMA busy of the shipped kernels from the committed SQ
     # counter passes of this config (tools/prof.sh -> tools/sqsum.py; PMC cannot run inside the bench)
     mfma_evidence = None
-    spath = os.path.join(ROOT, "profiles", f"r04_{args.config}_sq_counters.json")
-    if os.path.exists(spath):
+    def latest(stem):  # the newest round's committed profile of this config
+        for tag in ("r05", "r04"):
+            path = os.path.join(ROOT, "profiles", f"{tag}_{args.config}_{stem}.json")
+            if os.path.exists(path):
+                return path
+        return None
+    spath = latest("sq_counters")
+    if spath:
         sj = json.load(open(spath))
         mfma_evidence = {"source": os.path.relpath(spath, ROOT)}
         # the top-k scan's counters from the all-users profile when there is one (the sweep profile
         # scores a 16K-user sample)
-        tkp = os.path.join(ROOT, "profiles", f"r04_{args.config}_topk_sq_counters.json")
-        if os.path.exists(tkp):
+        tkp = latest("topk_sq_counters")
+        if tkp:
             sj = {k: v for k, v in sj.items() if not k.startswith("topk_scan_kernel")}
             sj.update({k: v for k, v in json.load(open(tkp)).items() if k.startswith("topk_scan_kernel")})
             mfma_evidence["source_topk"] = os.path.relpath(tkp, ROOT)
