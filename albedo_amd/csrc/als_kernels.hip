@@ -542,8 +542,8 @@ __global__ __launch_bounds__(64 * RBF_WAVES) void rotate_bf_kernel(const float* 
         }
     }
     if (t + tstep < ntile) xload(t + tstep, xn);
-    // output rows: lane l writes row r0 + (l >> 2), columns 16J + 4(l & 3) .. +3
-    const int orow = lane >> 2, oc = 4 * (lane & 3);
+    // output rows: lane l writes row r0 + (l & 15), columns 16J + 4(l >> 4) .. +3
+    const int orow = lane & 15, oc = 4 * (lane >> 4);  // 16 lanes: 16 rows of one 16-B unit (conflict-free reads)
     const int64_t rr = r0 + orow;
     // RBF_JU column blocks per step: their accumulator chains interleave (each chain keeps its own
     // product order, so Z is bit-identical to one block at a time)
