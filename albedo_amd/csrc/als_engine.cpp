@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdlib>
 #include <functional>
@@ -1574,9 +1575,22 @@ struct TopkPlan {
   // per call (topk_begin .. topk_finish): the passes run back to back with no host round trip; their
   // event pairs, scan counters (d_scan[pass]) and rows per scan workgroup are read at the end
   DevBuf d_cnt;  // int [4]: this pass's flagged count, the rescan work counter, the call's flagged total
-  std::vector<hipEvent_t> evs;  // 5 per pass: start, mask done, scan done, select done, rescans done
-  std::vector<int> pass_rpw;
+  // per pass: start, order + mask done, scan done, then per output range: select done, rescans done
+  std::vector<hipEvent_t> evs;
+  struct PassRec { int rpw; size_t e0; int ranges; };
+  std::vector<PassRec> passes;
   int64_t n_passes = 0;
+  DevBuf d_inv;  // output slot -> scan position of the current pass
+  hipError_t event(size_t i, hipEvent_t* e) {  // the i-th event of the pool (created on demand)
+    while (evs.size() <= i) {
+      hipEvent_t x;
+      const hipError_t r = hipEventCreate(&x);
+      if (r != hipSuccess) return r;
+      evs.push_back(x);
+    }
+    *e = evs[i];
+    return hipSuccess;
+  }
   ~TopkPlan() {
     for (hipEvent_t e : evs)
       if (e) (void)hipEventDestroy(e);
@@ -1695,25 +1709,28 @@ int topk_begin(als_ctx* c, TopkPlan& P, int64_t n_rows, int64_t n_passes, const 
   c->last_rescan.clear();
   c->last_rescan_ready = false;
   P.n_passes = n_passes;
-  P.pass_rpw.clear();
+  P.passes.clear();
   return ALS_OK;
 }
 
 int topk_finish(als_ctx* c, TopkPlan& P) {
   HIPCHK(hipStreamSynchronize(c->st));
-  const int64_t np = (int64_t)P.pass_rpw.size();
+  const int64_t np = (int64_t)P.passes.size();
   std::vector<unsigned long long> scanned((size_t)std::max<int64_t>(np, 1), 0ull);
   int cnt[4] = {0, 0, 0, 0};
   if (np > 0) HIPCHK(hipMemcpy(scanned.data(), P.d_scan.p, np * 8, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(cnt, P.d_cnt.p, 16, hipMemcpyDeviceToHost));
   for (int64_t q = 0; q < np; ++q) {
-    hipEvent_t* e = P.evs.data() + 5 * q;
+    const TopkPlan::PassRec& R = P.passes[q];
+    const hipEvent_t* e = P.evs.data() + R.e0;
     c->topk_ms[0] += event_ms(e[0], e[1]);
     c->topk_ms[1] += event_ms(e[1], e[2]);
-    c->topk_ms[2] += event_ms(e[2], e[3]);
-    c->topk_ms[3] += event_ms(e[3], e[4]);
+    for (int r = 0; r < R.ranges; ++r) {
+      c->topk_ms[2] += event_ms(r == 0 ? e[2] : e[3 + 2 * r - 1], e[3 + 2 * r]);
+      c->topk_ms[3] += event_ms(e[3 + 2 * r], e[4 + 2 * r]);
+    }
     c->topk_stats[2] += (int64_t)scanned[q];
-    c->topk_ms[4] += (double)scanned[q] * (P.pass_rpw[q] / 4) * 2.0 * c->KP;  // per wave: rpw / 4 src rows x each dst row
+    c->topk_ms[4] += (double)scanned[q] * (R.rpw / 4) * 2.0 * c->KP;  // per wave: rpw / 4 src rows x each dst row
   }
   c->topk_stats[1] += cnt[2];
   return ALS_OK;
@@ -1723,8 +1740,12 @@ int topk_finish(als_ctx* c, TopkPlan& P) {
 // generated on the device) at positions pos0 .. pos0 + nc - 1 of the call, into the device lists
 // d_oid / d_osc ([nc][k], score desc, id asc).  Rows that fail certification are compacted on the
 // device and re-scored by a persistent exact scan in the same stream: nothing here waits for the GPU.
+// After the scan the results are finished in output ranges of `range` rows (select, then the
+// rescans of the range); ready(o0, o1), when given, is called once a range's work is enqueued, so
+// the caller can copy those rows out while the next range computes.
+using TopkReady = std::function<int(int64_t, int64_t)>;
 int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t row0, int64_t pos0, int64_t nc, int32_t* d_oid,
-                  float* d_osc) {
+                  float* d_osc, int64_t range = INT64_MAX, const TopkReady& ready = nullptr) {
   Side& S = c->s[P.src];
   Side& T = c->s[1 - P.src];
   const int KP = c->KP, k = P.k;
@@ -1768,19 +1789,18 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t row0, in
     HIPCHK(P.d_kth.ensure(nc * 4));
     a.kth0 = P.d_kth.as<float>();
   }
-  const int64_t pass = (int64_t)P.pass_rpw.size();
+  const int64_t pass = (int64_t)P.passes.size();
   if (pass >= P.n_passes) return fail(ALS_E_STATE, "top-k: more passes than planned");
   a.scanned = P.d_scan.as<unsigned long long>() + pass;
   if (P.exact_only) {
     HIPCHK(launch_topk_exact(KP, a, nullptr, nc, c->st));
+    if (ready) TRYC(ready(0, nc));
     return ALS_OK;
   }
-  while ((int64_t)P.evs.size() < 5 * (pass + 1)) {
-    hipEvent_t e;
-    HIPCHK(hipEventCreate(&e));
-    P.evs.push_back(e);
-  }
-  hipEvent_t* ev = P.evs.data() + 5 * pass;
+  const int64_t nr = std::max<int64_t>(1, (nc + range - 1) / range);  // output ranges
+  const size_t e0 = P.evs.size();
+  hipEvent_t ev[3];
+  for (int i = 0; i < 3; ++i) HIPCHK(P.event(e0 + i, &ev[i]));
   // scan order: rows that stop at similar depths share a workgroup (topk_order); the select writes
   // each row's results back to its own slot
   TopkArgs b = a;
@@ -1811,14 +1831,39 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t row0, in
   HIPCHK(hipEventRecord(ev[1], c->st));
   HIPCHK(launch_topk(KP, b, c->n_cu, c->st));
   HIPCHK(hipEventRecord(ev[2], c->st));
-  HIPCHK(launch_topk_select(KP, b, c->st));
-  HIPCHK(hipEventRecord(ev[3], c->st));
-  // certification failures: compacted on the device (pass-local positions), re-scored in place
-  HIPCHK(hipMemsetAsync(P.d_cnt.p, 0, 8, c->st));  // this pass's count and work counter
+  if (nr > 1) {  // select by output slot: slot -> scan position
+    HIPCHK(P.d_inv.ensure(nc * 4));
+    HIPCHK(launch_invert_perm(b.out_pos, nc, P.d_inv.as<uint32_t>(), c->st));
+  }
   HIPCHK(P.d_flag.ensure(nc * 4));
-  HIPCHK(launch_topk_exact_flagged(KP, a, d_need, nc, P.d_flag.as<int32_t>(), P.d_cnt.as<int>(), c->n_cu, c->st));
-  HIPCHK(hipEventRecord(ev[4], c->st));
-  P.pass_rpw.push_back(rpw);
+  P.passes.push_back(TopkPlan::PassRec{rpw, e0, 0});
+  for (int64_t r = 0; r < nr; ++r) {
+    const int64_t o0 = r * range, n = std::min<int64_t>(range, nc - o0);
+    hipEvent_t es, ex;
+    HIPCHK(P.event(e0 + 3 + 2 * r, &es));
+    HIPCHK(P.event(e0 + 4 + 2 * r, &ex));
+    TopkArgs bs = b;
+    if (nr > 1) {
+      bs.in_pos = P.d_inv.as<uint32_t>();
+      bs.slot0 = o0;
+      bs.n_slots = n;
+    }
+    HIPCHK(launch_topk_select(KP, bs, c->st));
+    HIPCHK(hipEventRecord(es, c->st));
+    // certification failures of the range: compacted on the device (range-local positions), re-scored
+    // in place
+    TopkArgs ar = a;
+    ar.src_rows = a.src_rows + o0;
+    ar.out_ids = a.out_ids + o0 * k;
+    ar.out_scores = a.out_scores + o0 * k;
+    ar.kth0 = a.kth0 + o0;
+    ar.n_src = n;
+    HIPCHK(hipMemsetAsync(P.d_cnt.p, 0, 8, c->st));  // this range's count and work counter
+    HIPCHK(launch_topk_exact_flagged(KP, ar, d_need + o0, n, P.d_flag.as<int32_t>(), P.d_cnt.as<int>(), c->n_cu, c->st));
+    HIPCHK(hipEventRecord(ex, c->st));
+    P.passes.back().ranges = (int)(r + 1);
+    if (ready) TRYC(ready(o0, o0 + n));
+  }
   c->topk_stats[0] += nc;
   c->topk_stats[3] += (nc + rpw - 1) / rpw * 4 * P.n_chunks * P.CH;  // dst rows x waves
   return ALS_OK;
@@ -1891,32 +1936,73 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   c->last_rescan_ready = true;
   if (n_known == 0 || T.n == 0) return ALS_OK;
   stamp("host id mapping");
-  TopkPlan P;
-  TRYC(topk_plan(c, src, k, P));
-  stamp("plan (materialize dst, Gram + host eig, dst sort + fp16 pack)");
-  // 4M src rows per pass (candidate lists 4 GB): fewer launch tails than 1M-row passes
-  const int64_t chunk = 1 << 22;
+  // Src rows per pass: up to 2^25 (candidate lists 32 GiB of the 288 GB).  One scan launch over every
+  // row dispatches the heaviest workgroups (lowest relative thresholds) first and fills in behind
+  // them; split into 4M-row passes, each pass paid its own heavy tail (c4 all users: scan 436 ms in
+  // five passes, 260 ms in one; profiles/r05_bench_c4_topk_pass{4M,10M,20M}.json).  The results are
+  // finished and copied out in ranges of pass / 8 rows (at most 4M) while the next range computes.
+  // ALBEDO_TOPK_PASS (test knob): rows per pass.
+  const int64_t chunk = [] {
+    const char* e = std::getenv("ALBEDO_TOPK_PASS");
+    return e && *e ? std::max<int64_t>(1 << 16, std::atoll(e)) : (int64_t)1 << 25;
+  }();
+  const int64_t range = std::min<int64_t>((int64_t)1 << 22, std::max<int64_t>(chunk / 8, 1 << 16));
   // world > 1 (SURVEY §8(e) "Top-k: shard users"): rank r scores the r-th contiguous slice of the
   // known src rows against the replicated dst factors; the lists are all-gathered afterwards
   const int64_t per_rank = (n_known + c->world - 1) / c->world;
   const int64_t lo = std::min<int64_t>(n_known, (int64_t)c->rank * per_rank);
   const int64_t hi = std::min<int64_t>(n_known, lo + per_rank);
-  // dense output (every row of the side, the recommendForAll* case): the caller's arrays are pinned
-  // in place and each pass's lists go down on a copy stream while the next pass computes (two device
-  // buffers); elsewise (or if pinning fails) each pass is copied back before the next starts
-  bool async_out = false;
-  hipStream_t cs = nullptr;
-  hipEvent_t ev_comp[2] = {nullptr, nullptr}, ev_copy[2] = {nullptr, nullptr};
-  DevBuf d_oid2[2], d_osc2[2];
-  if (dense_out && hi > lo && hi - lo > chunk) {
-    const size_t bytes = (size_t)(hi - lo) * k * 4;
-    if (hipHostRegister(dst_ids_out + lo * k, bytes, hipHostRegisterDefault) == hipSuccess) {
-      if (hipHostRegister(scores_out + lo * k, bytes, hipHostRegisterDefault) == hipSuccess) async_out = true;
-      else (void)hipHostUnregister(dst_ids_out + lo * k);
+  std::vector<int64_t> pstart;  // pass starts
+  {
+    int64_t q = lo;
+    while (hi - q > chunk) {
+      pstart.push_back(q);
+      q += chunk;
     }
-    (void)hipGetLastError();  // a refused registration is not an error: the synchronous path runs
-    stamp("pin the output arrays");
+    if (q < hi) {
+      pstart.push_back(q);
+    }
   }
+  const int64_t n_pass = (int64_t)pstart.size();
+  // dense output (every row of the side, the recommendForAll* case): the caller's arrays are pinned
+  // in place (by a helper thread, while the plan runs) and each range's lists go down on a copy stream
+  // while the next range computes (two device buffers across passes); elsewise (or if pinning fails)
+  // each pass is copied back before the next starts
+  int pin_state = 0;  // bit 0: ids registered, bit 1: scores registered
+  const size_t pin_bytes = (size_t)(hi - lo) * k * 4;
+  auto pin = [&, dev = c->dev]() {
+    if (hipSetDevice(dev) != hipSuccess) return;
+    if (hipHostRegister(dst_ids_out + lo * k, pin_bytes, hipHostRegisterDefault) != hipSuccess) return;
+    pin_state |= 1;
+    if (hipHostRegister(scores_out + lo * k, pin_bytes, hipHostRegisterDefault) == hipSuccess) pin_state |= 2;
+  };
+  std::thread pin_thr;
+  const bool want_pin = dense_out && hi - lo > range;
+  if (want_pin) {
+    try {
+      pin_thr = std::thread(pin);
+    } catch (const std::system_error&) {
+      pin();  // no thread: pin here
+    }
+  }
+  TopkPlan P;
+  const int plan_rc = topk_plan(c, src, k, P);
+  if (pin_thr.joinable()) pin_thr.join();
+  (void)hipGetLastError();  // a refused registration is not an error: the synchronous path runs
+  if (pin_state == 1) (void)hipHostUnregister(dst_ids_out + lo * k);
+  bool async_out = pin_state == 3;
+  if (plan_rc != ALS_OK) {
+    if (async_out) {
+      (void)hipHostUnregister(dst_ids_out + lo * k);
+      (void)hipHostUnregister(scores_out + lo * k);
+    }
+    return plan_rc;
+  }
+  stamp("plan (materialize dst, Gram + host eig, dst sort + fp16 pack) + pin the output arrays");
+  hipStream_t cs = nullptr;
+  hipEvent_t ev_copy[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> ev_rng;  // one per finished range: the copy stream waits for it
+  DevBuf d_oid2[2], d_osc2[2];
   // releases everything the async path holds (null-safe: also after a partial set-up)
   auto end_async = [&]() {
     if (!async_out) return;
@@ -1925,10 +2011,11 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
     (void)hipHostUnregister(dst_ids_out + lo * k);
     (void)hipHostUnregister(scores_out + lo * k);
     for (int b = 0; b < 2; ++b) {
-      if (ev_comp[b]) (void)hipEventDestroy(ev_comp[b]);
       if (ev_copy[b]) (void)hipEventDestroy(ev_copy[b]);
-      ev_comp[b] = ev_copy[b] = nullptr;
+      ev_copy[b] = nullptr;
     }
+    for (hipEvent_t e : ev_rng) (void)hipEventDestroy(e);
+    ev_rng.clear();
     if (cs) (void)hipStreamDestroy(cs);
     cs = nullptr;
     async_out = false;
@@ -1936,11 +2023,8 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   if (async_out) {  // the copy stream and its events; if any cannot be created, the synchronous path runs
     bool ok = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) == hipSuccess;
     if (!ok) cs = nullptr;
-    for (int b = 0; b < 2 && ok; ++b) {
-      ok = hipEventCreateWithFlags(&ev_comp[b], hipEventDisableTiming) == hipSuccess;
-      if (!ok) ev_comp[b] = nullptr;
-      else if (!(ok = hipEventCreateWithFlags(&ev_copy[b], hipEventDisableTiming) == hipSuccess)) ev_copy[b] = nullptr;
-    }
+    for (int b = 0; b < 2 && ok; ++b)
+      if (!(ok = hipEventCreateWithFlags(&ev_copy[b], hipEventDisableTiming) == hipSuccess)) ev_copy[b] = nullptr;
     if (!ok) {
       end_async();
       (void)hipGetLastError();
@@ -1948,27 +2032,36 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   }
   DevBuf d_oid, d_osc;
   {
-    const int rc = topk_begin(c, P, n_known, (hi - lo + chunk - 1) / chunk, all_rows ? nullptr : known.data());
+    const int rc = topk_begin(c, P, n_known, n_pass, all_rows ? nullptr : known.data());
     if (rc != ALS_OK) {
       end_async();
       return rc;
     }
   }
-  for (int64_t q0 = lo, it = 0; q0 < hi; q0 += chunk, ++it) {
-    const int64_t nc = std::min<int64_t>(chunk, hi - q0);
+  for (int64_t it = 0; it < n_pass; ++it) {
+    const int64_t q0 = pstart[it], nc = (it + 1 < n_pass ? pstart[it + 1] : hi) - q0;
     if (async_out) {
       const int b = (int)(it & 1);
       int rc = ALS_OK;
       if (it >= 2 && hipStreamWaitEvent(c->st, ev_copy[b], 0) != hipSuccess) rc = fail(ALS_E_HIP, "stream wait");
       if (rc == ALS_OK && (d_oid2[b].ensure(nc * k * 4) != hipSuccess || d_osc2[b].ensure(nc * k * 4) != hipSuccess))
         rc = fail(ALS_E_OUT_OF_MEMORY, "top-k output buffers");
-      if (rc == ALS_OK) rc = topk_run_rows(c, P, rowsf(q0), q0, q0, nc, d_oid2[b].as<int32_t>(), d_osc2[b].as<float>());
-      if (rc == ALS_OK &&
-          (hipEventRecord(ev_comp[b], c->st) != hipSuccess || hipStreamWaitEvent(cs, ev_comp[b], 0) != hipSuccess ||
-           hipMemcpyAsync(dst_ids_out + q0 * k, d_oid2[b].p, nc * k * 4, hipMemcpyDeviceToHost, cs) != hipSuccess ||
-           hipMemcpyAsync(scores_out + q0 * k, d_osc2[b].p, nc * k * 4, hipMemcpyDeviceToHost, cs) != hipSuccess ||
-           hipEventRecord(ev_copy[b], cs) != hipSuccess))
-        rc = fail(ALS_E_HIP, "top-k result copy");
+      // each finished range of the pass goes down on the copy stream
+      const TopkReady copy_out = [&, b, q0](int64_t o0, int64_t o1) -> int {
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(ALS_E_HIP, "top-k copy event");
+        ev_rng.push_back(e);
+        if (hipEventRecord(e, c->st) != hipSuccess || hipStreamWaitEvent(cs, e, 0) != hipSuccess ||
+            hipMemcpyAsync(dst_ids_out + (q0 + o0) * k, d_oid2[b].as<int32_t>() + o0 * k, (o1 - o0) * k * 4,
+                           hipMemcpyDeviceToHost, cs) != hipSuccess ||
+            hipMemcpyAsync(scores_out + (q0 + o0) * k, d_osc2[b].as<float>() + o0 * k, (o1 - o0) * k * 4,
+                           hipMemcpyDeviceToHost, cs) != hipSuccess)
+          return fail(ALS_E_HIP, "top-k result copy");
+        return ALS_OK;
+      };
+      if (rc == ALS_OK)
+        rc = topk_run_rows(c, P, rowsf(q0), q0, q0, nc, d_oid2[b].as<int32_t>(), d_osc2[b].as<float>(), range, copy_out);
+      if (rc == ALS_OK && hipEventRecord(ev_copy[b], cs) != hipSuccess) rc = fail(ALS_E_HIP, "top-k result copy");
       if (rc != ALS_OK) {
         end_async();
         return rc;
@@ -2084,7 +2177,7 @@ int als_evaluate_ndcg(als_ctx* c, int32_t k, int64_t n, const int32_t* user, con
   TRYC(topk_plan(c, ALS_USER, k, P));
   const int64_t per_rank = (nr + c->world - 1) / c->world;
   const int64_t lo = std::min<int64_t>(nr, (int64_t)c->rank * per_rank), hi = std::min<int64_t>(nr, lo + per_rank);
-  const int64_t chunk = 1 << 20;
+  const int64_t chunk = 1 << 25;  // one pass for any realistic user count (see als_recommend)
   DevBuf d_oid, d_osc;
   TRYC(topk_begin(c, P, nr, (hi - lo + chunk - 1) / chunk, rows.data()));
   for (int64_t q0 = lo; q0 < hi; q0 += chunk) {

@@ -172,6 +172,10 @@ struct TopkArgs {
   unsigned long long* scanned;  // += dst chunks scanned by each scan workgroup (or null)
   const uint32_t* out_pos;      // select: results of scan position i go to slot out_pos[i] (or i)
   const float* thr0;            // scan: starting threshold of each src position (topk_order; or null)
+  // select over output slots slot0 .. slot0 + n_slots - 1 (in_pos != null: slot -> scan position,
+  // the inverse of out_pos), so a pass's results can be finished and copied out range by range
+  const uint32_t* in_pos;
+  int64_t slot0, n_slots;
 };
 constexpr int TOPK_KC = 64;     // candidates rescored exactly per src row (k <= 64)
 constexpr int TOPK_CAP = 128;   // candidate list capacity per src row (compacted to 64 above TOPK_TRIG)
@@ -200,6 +204,8 @@ hipError_t launch_topk_mask(const TopkArgs& a, int rows_per_wg, const float* sup
 int topk_rows_per_workgroup(int KP, int64_t n_src, int n_cu);
 // exact full scan for the given src-row indices (rows == null: rows 0 .. n_rows-1), any k <= TOPK_MAX
 hipError_t launch_topk_exact(int KP, const TopkArgs& a, const int32_t* rows, int64_t n_rows, hipStream_t s);
+// inv[perm[i]] = i for i < n
+hipError_t launch_invert_perm(const uint32_t* perm, int64_t n, uint32_t* inv, hipStream_t s);
 hipError_t launch_iota_i32(int32_t* out, int64_t n, int64_t start, hipStream_t s);  // out[i] = start + i
 // the certification rescans without a host round trip: need[0 .. n) compacted into flags (cnt[0]: their
 // count, cnt[1]: the persistent grid's work counter, both zero on entry; cnt[2] += the count), then a

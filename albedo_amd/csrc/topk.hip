@@ -599,9 +599,17 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
   constexpr int CAP = TOPK_CAP, NS = CAP / 64;
   __shared__ __attribute__((aligned(16))) float s_stage[4][64 * TK_SEL_LD + KP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t si = (int64_t)blockIdx.x * 4 + wave;
-  if (si >= a.n_src) return;
-  const int64_t so = a.out_pos ? (int64_t)a.out_pos[si] : si;  // output slot of scan position si
+  int64_t si, so;  // scan position, output slot
+  if (a.in_pos) {  // a range of output slots
+    const int64_t l = (int64_t)blockIdx.x * 4 + wave;
+    if (l >= a.n_slots) return;
+    so = a.slot0 + l;
+    si = a.in_pos[so];
+  } else {
+    si = (int64_t)blockIdx.x * 4 + wave;
+    if (si >= a.n_src) return;
+    so = a.out_pos ? (int64_t)a.out_pos[si] : si;
+  }
   const int srow = a.src_rows[si];
   const float* s = a.S + (int64_t)srow * KP;
   const int cnt = min(a.lcnt[si], CAP);
@@ -1257,8 +1265,9 @@ extern "C" int als_debug_topk_phases(unsigned long long* out16, int reset) {
 #endif
 
 hipError_t launch_topk_select(int KP, const TopkArgs& a, hipStream_t s) {
-  if (a.n_src <= 0) return hipSuccess;
-  const int blocks = (int)((a.n_src + 3) / 4);
+  const int64_t n = a.in_pos ? a.n_slots : a.n_src;
+  if (n <= 0) return hipSuccess;
+  const int blocks = (int)((n + 3) / 4);
   if (KP == 64) topk_select_kernel<64><<<blocks, 256, 0, s>>>(a);
   else if (KP == 128) topk_select_kernel<128><<<blocks, 256, 0, s>>>(a);
   else if (KP == 256) topk_select_kernel<256><<<blocks, 256, 0, s>>>(a);
@@ -1336,6 +1345,16 @@ hipError_t launch_topk_exact_flagged(int KP, const TopkArgs& a, const int32_t* n
   if (KP == 128) return topk_exact_dev_p<128, 1>(a, flags, dcount, dnext, grid, s);
   if (KP == 256) return topk_exact_dev_p<256, 1>(a, flags, dcount, dnext, grid, s);
   return hipErrorInvalidValue;
+}
+
+__global__ void invert_perm_kernel(const uint32_t* __restrict__ perm, int64_t n, uint32_t* __restrict__ inv) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    inv[perm[i]] = (uint32_t)i;
+}
+hipError_t launch_invert_perm(const uint32_t* perm, int64_t n, uint32_t* inv, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  invert_perm_kernel<<<tk_grid(n, 256), 256, 0, s>>>(perm, n, inv);
+  return hipGetLastError();
 }
 
 __global__ void iota_i32_kernel(int32_t* __restrict__ out, int64_t n, int64_t start) {

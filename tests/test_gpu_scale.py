@@ -156,6 +156,35 @@ def test_c3_topk_all_users_after_10_sweeps(gpu_lib, c2_ctx):
     print("c3 top-30:", r)
 
 
+def _recommend_all(gpu_lib, c, k):
+    from albedo_amd import _lib as L
+    n_u = gpu_lib.als_num_rows(c.h, 0)
+    ids = np.empty((n_u, k), np.int32)
+    sc = np.empty((n_u, k), np.float32)
+    L.check(gpu_lib.als_recommend(c.h, 0, k, None, n_u, None, L.ptr(ids, C.c_int32), L.ptr(sc, C.c_float)))
+    n_res = np.zeros(1, np.int64)
+    L.check(gpu_lib.als_topk_last_rescan(c.h, None, 0, L.ptr(n_res, C.c_int64)))
+    resc = np.empty(max(int(n_res[0]), 1), np.int32)
+    L.check(gpu_lib.als_topk_last_rescan(c.h, L.ptr(resc, C.c_int32), resc.size, L.ptr(n_res, C.c_int64)))
+    return ids, sc, np.sort(resc[:int(n_res[0])])
+
+
+@pytest.mark.timeout(400)
+def test_c3_topk_passes_and_ranges_identical(gpu_lib, c2_ctx, monkeypatch):
+    """recommendForAllUsers(30) over the 1M c3 users in one pass (the default: one scan launch, the
+    results finished and copied out in ranges) and in passes of 300K rows (ALBEDO_TOPK_PASS; four
+    passes, each finished in four 64K-row ranges plus a remainder): the same lists and the same score
+    bits (which rows need the exact rescan may differ: a row's scan workgroup, and so the chunks it is
+    scored against, depends on the pass it sorts in)."""
+    c = c2_ctx
+    ids1, sc1, r1 = _recommend_all(gpu_lib, c, 30)
+    monkeypatch.setenv("ALBEDO_TOPK_PASS", "300000")
+    ids2, sc2, r2 = _recommend_all(gpu_lib, c, 30)
+    assert np.array_equal(ids1, ids2)
+    assert np.array_equal(sc1.view(np.uint32), sc2.view(np.uint32))
+    print("c3 rescans: one pass", r1.size, "300K-row passes", r2.size)
+
+
 @pytest.mark.timeout(600)
 def test_c4_scale_rows_match_fp64_solve(gpu_lib, c4_ctx):
     """Full-size property at BASELINE config 4 (20M x 4M, 1B stars, rank 128; the bench workload):

@@ -14,6 +14,7 @@ for s in "$@"; do
     tests_quick) timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "half_sweep or golden or facade or albedo_protocol" > gpurun_out/tests_quick.log 2>&1 ;;
     tests_topk) timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_recommenders.py -k "topk or ndcg or recommend or transform or facade or albedo" > gpurun_out/tests_topk.log 2>&1 ;;
     tests_scale) timeout -k 10 900 $PYT tests/test_gpu_scale.py -s > gpurun_out/tests_scale.log 2>&1 ;;
+    tests_c3) timeout -k 10 600 $PYT tests/test_gpu_scale.py -s -k "c2_scale or c3" > gpurun_out/tests_c3.log 2>&1 ;;
     tests_all) timeout -k 10 1100 $PYT tests -m gpu > gpurun_out/tests_all.log 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke.log 2>&1 ;;
     bench_c4) timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_c4.json 2> gpurun_out/bench_c4.err ;;
@@ -51,6 +52,7 @@ for s in "$@"; do
     bench_topk_g4) ALBEDO_TOPK_GMAX=4 timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk_g4.json 2> gpurun_out/bench_topk_g4.err ;;
     topkph_g4) ALBEDO_TOPK_GMAX=4 timeout -k 10 400 python -u tools/topk_phases.py --lib tools/ab/topkph.so --out gpurun_out/topkph_g4.json > gpurun_out/topkph_g4.log 2>&1 ;;
     bench_topk_tr) ALBEDO_TOPK_TRACE=1 timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk_tr.json 2> gpurun_out/bench_topk_tr.err ;;
+    bench_topk_p*) ALBEDO_TOPK_PASS=${s#bench_topk_p} timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
     bench_topk) timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk.json 2> gpurun_out/bench_topk.err ;;
     bench_c4q) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 > gpurun_out/bench_c4q.json 2> gpurun_out/bench_c4q.err ;;
     bench_c4q_l*) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 --light ${s#bench_c4q_l} > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
