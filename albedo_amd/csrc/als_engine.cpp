@@ -1781,6 +1781,10 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t row0, in
   a.scaled = (float)(P.ssc * P.tsc);
   a.lent = P.d_ls.as<uint2>();
   a.lcnt = P.d_lc.as<int32_t>();
+  // scan order: 12 bits of depth, then 7 / 7 / 6 bits of direction (topk_order_key_kernel; c4 all
+  // users: scan 260 -> 193 ms, order + mask 56 -> 39 ms against the depth-only key; 18 / 22 / 24
+  // direction bits 206 / 206 / 276 ms, other splits of 20 the same 193)
+  a.order_dir_bits = 7 | (7 << 8) | (6 << 16);
   a.out_ids = d_oid;
   a.out_scores = d_osc;
   int32_t* d_need = c->d_last_need.as<int32_t>() + pos0;

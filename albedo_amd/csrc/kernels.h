@@ -176,6 +176,7 @@ struct TopkArgs {
   // the inverse of out_pos), so a pass's results can be finished and copied out range by range
   const uint32_t* in_pos;
   int64_t slot0, n_slots;
+  int order_dir_bits;           // order: key bits of the direction s_P / ‖s‖ (bytes: u1, u2, u3; 0: depth only)
 };
 constexpr int TOPK_KC = 64;     // candidates rescored exactly per src row (k <= 64)
 constexpr int TOPK_CAP = 128;   // candidate list capacity per src row (compacted to 64 above TOPK_TRIG)

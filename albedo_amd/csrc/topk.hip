@@ -12,7 +12,8 @@
 //           largest-norm rows;
 //  order    one wave per 16 src rows: scores against the probe rows on MFMA, the kt-th best v* -> the
 //           starting threshold thr0 = v* minus the rounding difference to the scan; the src features
-//           (s_P, ‖s_⊥‖, the pruning margin); a sort key that groups rows of similar depth;
+//           (s_P, ‖s_⊥‖, the pruning margin); a sort key that groups rows of similar depth and
+//           direction;
 //  mask     per scan workgroup, the chunks any of its rows can still need against thr0 (super-chunks
 //           first): a bitmask;
 //  scan     one workgroup per 64·G src rows over the masked chunks: the src rows' fp16 fragments stay in
@@ -678,7 +679,7 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
 // dst Gram's leading eigenvectors, rounded), ‖s_⊥‖ (rounded up, with a floor for the fp64 cancellation),
 // the pruning margin e + 1.2e-5·‖s‖·max‖t‖ (e: select's approx error; 1.2e-5 covers the fp32 bound
 // arithmetic and F2J's own rounding), ‖s‖ rounded up.  Sort key: thr0 / ‖s‖ (rows that stop at
-// similar depths share a workgroup).
+// similar depths share a workgroup), its low a.order_dir_bits bits replaced by the direction of s_P.
 template <int KP>
 __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_t* __restrict__ key,
                                                              uint32_t* __restrict__ val, float* __restrict__ thr0,
@@ -770,7 +771,22 @@ __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_
       thr0[pr] = t0;
       const float k = nrm > 0.0 ? (float)((double)t0 / nrm) : INFINITY;
       const uint32_t bb = __float_as_uint(k);
-      key[pr] = (bb & 0x80000000u) ? ~bb : (bb | 0x80000000u);
+      uint32_t kk32 = (bb & 0x80000000u) ? ~bb : (bb | 0x80000000u);
+      if (a.order_dir_bits != 0 && nrm > 0.0) {
+        // coarser depth, then the direction of s_P (lexicographic in u1, u2, u3 = s_P[1..3] / ‖s‖):
+        // the rows of one workgroup then need similar chunks, so its mask union stays tight and its
+        // waves skip fewer of the chunks it streams
+        const int b1 = a.order_dir_bits & 255, b2 = (a.order_dir_bits >> 8) & 255, b3 = (a.order_dir_bits >> 16) & 255;
+        const int db = b1 + b2 + b3;
+        auto qz = [](double u, int bits) {
+          const int m = (1 << bits) - 1;
+          const int v = (int)((u + 1.0) * 0.5 * (double)(m + 1));
+          return (uint32_t)(v < 0 ? 0 : (v > m ? m : v));
+        };
+        const uint32_t code = (qz(sq[1] / nrm, b1) << (b2 + b3)) | (qz(sq[2] / nrm, b2) << b3) | qz(sq[3] / nrm, b3);
+        kk32 = (kk32 & ~((1u << db) - 1u)) | code;
+      }
+      key[pr] = kk32;
       val[pr] = (uint32_t)pr;
       float* o = sfo + pr * TOPK_SF;
 #pragma unroll

@@ -1,0 +1,73 @@
+"""Probe (not a test): run-to-run identity of the fit at a BASELINE config, two contexts in one process.
+
+  python tools/determinism.py [--config c2] [--rank 64] [--halves 20] [--out gpurun_out/det.json]
+
+Ingests the synthetic config into two contexts (the device generator), checks that both see the
+same ratings (degrees of every row), initialises both (Spark-style init) and runs item / user
+half-sweeps side by side, comparing the new factors bit for bit after every half.  On the first
+difference it reports which rows differ, their degrees (the degree selects the solve path: light16
+d <= 16, light 17..64, wave kernel above, split-K above the split chunk) and the size of the
+difference, then stops.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--rank", type=int, default=64)
+    ap.add_argument("--halves", type=int, default=20)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    from albedo_amd import _lib as L
+    from tests.test_gpu_scale import _ingest
+    lib = L.load()
+    a = _ingest(lib, args.config, args.rank)
+    b = _ingest(lib, args.config, args.rank)
+    rep = {"config": args.config, "rank": args.rank}
+    deg = {}
+    for side in (0, 1):
+        d = [np.empty(lib.als_num_rows(c.h, side), np.int64) for c in (a, b)]
+        for c, x in zip((a, b), d):
+            L.check(lib.als_get_degrees(c.h, side, L.ptr(x, C.c_int64)))
+        rep[f"same_degrees_side{side}"] = bool(np.array_equal(d[0], d[1]))
+        deg[side] = d[0]
+    ua, ub = a.factors(0)[1], b.factors(0)[1]
+    rep["same_init"] = bool(np.array_equal(ua.view(np.uint32), ub.view(np.uint32)))
+    rep["halves"] = []
+    for h in range(args.halves):
+        side = 1 if h % 2 == 0 else 0  # item half first (Spark's order)
+        a.half(side)
+        b.half(side)
+        fa, fb = a.factors(side)[1], b.factors(side)[1]
+        diff = np.any(fa.view(np.uint32) != fb.view(np.uint32), axis=1)
+        n = int(diff.sum())
+        rec = {"half": h, "side": "item" if side == 1 else "user", "rows_differ": n}
+        if n:
+            rows = np.nonzero(diff)[0]
+            dd = deg[side][rows]
+            rel = np.max(np.abs(fa[rows] - fb[rows]), axis=1) / np.maximum(np.max(np.abs(fa[rows]), axis=1), 1e-30)
+            rec.update(first_rows=rows[:20].tolist(), degrees=dd[:20].tolist(), rel=rel[:20].tolist(),
+                       degree_hist={"<=8": int((dd <= 8).sum()), "9-16": int(((dd > 8) & (dd <= 16)).sum()),
+                                    "17-64": int(((dd > 16) & (dd <= 64)).sum()), ">64": int((dd > 64).sum())},
+                       max_rel=float(rel.max()))
+        rep["halves"].append(rec)
+        print(json.dumps(rec), flush=True)
+        if n:
+            break
+    if args.out:
+        json.dump(rep, open(args.out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in rep.items() if k != "halves"}))
+
+
+if __name__ == "__main__":
+    main()

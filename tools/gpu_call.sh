@@ -29,6 +29,8 @@ for s in "$@"; do
     pmc_topk5) timeout -k 10 700 tools/pmc_topk5.sh r05 > gpurun_out/pmc_topk5.log 2>&1 ;;
     multi) # back-to-back processes on one box (each a fresh context on memory the previous one freed)
       for i in 1 2 3 4 5 6; do timeout -k 10 200 python -u bench.py --steps 2 --warmup 40 --no-cpu --topk-users 0 > gpurun_out/multi_$i.json 2> gpurun_out/multi_$i.err || { echo "multi run $i failed"; exit 1; }; done ;;
+    det_c2) timeout -k 10 300 python -u tools/determinism.py --config c2 --rank 64 --halves 20 --out gpurun_out/det_c2.json > gpurun_out/det_c2.log 2>&1 ;;
+    det_c4) timeout -k 10 400 python -u tools/determinism.py --config c4 --rank 128 --halves 12 --out gpurun_out/det_c4.json > gpurun_out/det_c4.log 2>&1 ;;
     stress) timeout -k 10 300 python -u bench.py --steps 5 --warmup 300 --no-cpu --topk-users 0 > gpurun_out/stress.json 2> gpurun_out/stress.err ;;
     prof_c5) timeout -k 10 900 tools/prof.sh c5 r03 0 > gpurun_out/prof_c5.log 2>&1 ;;
     prof_c2) timeout -k 10 600 tools/prof.sh c2 r03 16384 > gpurun_out/prof_c2.log 2>&1 ;;
@@ -53,6 +55,7 @@ for s in "$@"; do
     topkph_g4) ALBEDO_TOPK_GMAX=4 timeout -k 10 400 python -u tools/topk_phases.py --lib tools/ab/topkph.so --out gpurun_out/topkph_g4.json > gpurun_out/topkph_g4.log 2>&1 ;;
     bench_topk_tr) ALBEDO_TOPK_TRACE=1 timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk_tr.json 2> gpurun_out/bench_topk_tr.err ;;
     bench_topk_p*) ALBEDO_TOPK_PASS=${s#bench_topk_p} timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
+    bench_topk_d*) ALBEDO_TOPK_DIRSPLIT=${s#bench_topk_d} timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
     bench_topk) timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk.json 2> gpurun_out/bench_topk.err ;;
     bench_c4q) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 > gpurun_out/bench_c4q.json 2> gpurun_out/bench_c4q.err ;;
     bench_c4q_l*) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 --light ${s#bench_c4q_l} > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
