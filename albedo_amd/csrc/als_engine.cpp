@@ -206,6 +206,22 @@ int set_device(als_ctx* c) {
   return ALS_OK;
 }
 
+// Copies and fills between the host and the context's buffers go through the engine stream c->st and
+// complete before returning.  c->st is a non-blocking stream: it does not order itself after the null
+// stream, so a plain hipMemcpy / hipMemset could overlap the engine's kernels (a host-to-device
+// hipMemcpy from pageable memory may return before its DMA lands, a device-to-device one does not
+// wait at all, and neither waits for kernels still running on c->st).
+hipError_t copy_st(const als_ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+  if (bytes == 0) return hipSuccess;
+  const hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, c->st);
+  return e != hipSuccess ? e : hipStreamSynchronize(c->st);
+}
+hipError_t fill_st(const als_ctx* c, void* dst, int v, size_t bytes) {
+  if (bytes == 0) return hipSuccess;
+  const hipError_t e = hipMemsetAsync(dst, v, bytes, c->st);
+  return e != hipSuccess ? e : hipStreamSynchronize(c->st);
+}
+
 // world > 1: the factor-chunk gathers of the last half-sweep run on st2 behind the solve.  Anything
 // that rewrites factor buffers with default-stream copies, or returns to the caller as "done",
 // first waits for both streams.
@@ -414,7 +430,7 @@ int rank_layout(als_ctx* c) {
     }
     S.boff[NBUCKET] = (int64_t)all.size();
     HIPCHK(S.d_rows.ensure(all.size() * 4));
-    HIPCHK(hipMemcpy(S.d_rows.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(copy_st(c, S.d_rows.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(S.d_desc.ensure(all.size() * 16));
     HIPCHK(launch_row_desc(S.d_rows.as<int32_t>(), (int64_t)all.size(), S.d_ptr.as<int64_t>(), S.d_desc.as<int32_t>(), c->st));
     HIPCHK(hipStreamSynchronize(c->st));
@@ -448,9 +464,9 @@ int rank_layout(als_ctx* c) {
       HIPCHK(S.d_chunk_row.ensure(crow.size() * 4));
       HIPCHK(S.d_chunk_idx.ensure(cidx.size() * 4));
       HIPCHK(S.d_slot0.ensure(slot0.size() * 4));
-      HIPCHK(hipMemcpy(S.d_chunk_row.p, crow.data(), crow.size() * 4, hipMemcpyHostToDevice));
-      HIPCHK(hipMemcpy(S.d_chunk_idx.p, cidx.data(), cidx.size() * 4, hipMemcpyHostToDevice));
-      HIPCHK(hipMemcpy(S.d_slot0.p, slot0.data(), slot0.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(copy_st(c, S.d_chunk_row.p, crow.data(), crow.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(copy_st(c, S.d_chunk_idx.p, cidx.data(), cidx.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(copy_st(c, S.d_slot0.p, slot0.data(), slot0.size() * 4, hipMemcpyHostToDevice));
     }
   }
   return factor_buffers(c);
@@ -474,11 +490,11 @@ int factor_buffers(als_ctx* c) {
     HIPCHK(S.d_X.ensure((size_t)std::max<int64_t>(std::max<int64_t>(S.own_n, (int64_t)S.nch * S.chpad), 1) * c->KP * 4));
     // + one zero row at prows(): the gather target of masked light-row entries (never written)
     HIPCHK(S.d_Z.ensure((size_t)(S.prows() + 1) * c->KP * 4));
-    HIPCHK(hipMemset(S.d_X.p, 0, S.d_X.bytes));
-    HIPCHK(hipMemset(S.d_Z.p, 0, S.d_Z.bytes));
+    HIPCHK(fill_st(c, S.d_X.p, 0, S.d_X.bytes));
+    HIPCHK(fill_st(c, S.d_Z.p, 0, S.d_Z.bytes));
     if (c->world > 1) {
       HIPCHK(S.d_Xfull.ensure((size_t)std::max<int64_t>(S.prows(), 1) * c->KP * 4));
-      HIPCHK(hipMemset(S.d_Xfull.p, 0, S.d_Xfull.bytes));
+      HIPCHK(fill_st(c, S.d_Xfull.p, 0, S.d_Xfull.bytes));
     }
     S.full_valid = false;
     HIPCHK(S.d_B.ensure((size_t)c->KP * c->KP * 8));
@@ -532,8 +548,8 @@ int ingest_device(als_ctx* c, int64_t n, const int32_t* d_user, const int32_t* d
   I.n = ni;
   U.ids.resize(nu);
   I.ids.resize(ni);
-  HIPCHK(hipMemcpy(U.ids.data(), uu, nu * 4, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(I.ids.data(), ii, ni * 4, hipMemcpyDeviceToHost));
+  HIPCHK(copy_st(c, U.ids.data(), uu, nu * 4, hipMemcpyDeviceToHost));
+  HIPCHK(copy_st(c, I.ids.data(), ii, ni * 4, hipMemcpyDeviceToHost));
   (void)hipFree(uu);
   (void)hipFree(ii);
   c->nnz = n;
@@ -550,7 +566,7 @@ int ingest_device(als_ctx* c, int64_t n, const int32_t* d_user, const int32_t* d
     HIPCHK(build_csr(dst, src, d_rating, n, S.n, c->s[1 - side].n, F.ptr.as<int64_t>(), F.col.as<int32_t>(),
                      F.val.as<float>(), st));
     F.hptr.resize(S.n + 1);
-    HIPCHK(hipMemcpy(F.hptr.data(), F.ptr.p, (S.n + 1) * 8, hipMemcpyDeviceToHost));
+    HIPCHK(copy_st(c, F.hptr.data(), F.ptr.p, (S.n + 1) * 8, hipMemcpyDeviceToHost));
     S.starts.assign(c->world + 1, 0);
     plan_shards(F.hptr.data(), S.n, c->world, S.starts.data());
     S.maxrows = 0;
@@ -572,12 +588,12 @@ int ingest_device(als_ctx* c, int64_t n, const int32_t* d_user, const int32_t* d
     std::vector<int64_t> lp(S.own_n + 1);
     for (int64_t r = 0; r <= S.own_n; ++r) lp[r] = F.hptr[S.own0 + r] - e0;
     HIPCHK(S.d_ptr.ensure((S.own_n + 1) * 8));
-    HIPCHK(hipMemcpy(S.d_ptr.p, lp.data(), (S.own_n + 1) * 8, hipMemcpyHostToDevice));
+    HIPCHK(copy_st(c, S.d_ptr.p, lp.data(), (S.own_n + 1) * 8, hipMemcpyHostToDevice));
     HIPCHK(S.d_col.ensure(S.own_nnz * 4));
     HIPCHK(S.d_val.ensure(S.own_nnz * 4));
-    HIPCHK(hipMemcpy(S.d_val.p, F.val.as<float>() + e0, S.own_nnz * 4, hipMemcpyDeviceToDevice));
+    HIPCHK(copy_st(c, S.d_val.p, F.val.as<float>() + e0, S.own_nnz * 4, hipMemcpyDeviceToDevice));
     if (c->world == 1) {
-      HIPCHK(hipMemcpy(S.d_col.p, F.col.as<int32_t>() + e0, S.own_nnz * 4, hipMemcpyDeviceToDevice));
+      HIPCHK(copy_st(c, S.d_col.p, F.col.as<int32_t>() + e0, S.own_nnz * 4, hipMemcpyDeviceToDevice));
     } else {  // dense src index -> padded src position, on the device
       ShardStarts ss{};
       ss.world = c->world;
@@ -610,7 +626,7 @@ int upload_factors(als_ctx* c, int side, const float* f, int64_t ld) {
   std::vector<float> h((size_t)std::max<int64_t>(S.own_n, 1) * c->KP, 0.f);
   for (int64_t r = 0; r < S.own_n; ++r)
     std::memcpy(&h[(size_t)r * c->KP], f + (size_t)(S.own0 + r) * ld, sizeof(float) * c->p.rank);
-  HIPCHK(hipMemcpy(S.d_X.p, h.data(), (size_t)S.own_n * c->KP * 4, hipMemcpyHostToDevice));
+  HIPCHK(copy_st(c, S.d_X.p, h.data(), (size_t)S.own_n * c->KP * 4, hipMemcpyHostToDevice));
   HIPCHK(launch_identity(S.d_B.as<double>(), c->KP, c->st));
   S.has_factors = true;
   S.orig_valid = false;
@@ -1357,9 +1373,9 @@ int als_set_ratings(als_ctx* c, int64_t n, const int32_t* user, const int32_t* i
   HIPCHK(du.ensure(n * 4));
   HIPCHK(di.ensure(n * 4));
   HIPCHK(dr.ensure(n * 4));
-  HIPCHK(hipMemcpy(du.p, user, n * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(di.p, item, n * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(dr.p, rating, n * 4, hipMemcpyHostToDevice));
+  HIPCHK(copy_st(c, du.p, user, n * 4, hipMemcpyHostToDevice));
+  HIPCHK(copy_st(c, di.p, item, n * 4, hipMemcpyHostToDevice));
+  HIPCHK(copy_st(c, dr.p, rating, n * 4, hipMemcpyHostToDevice));
   return ingest_device(c, n, du.as<int32_t>(), di.as<int32_t>(), dr.as<float>());
 }
 
@@ -1506,7 +1522,7 @@ int als_get_factors(als_ctx* c, int side, int32_t* ids_out, float* f_out) {
   if (f_out) {
     const int KP = c->KP, k = c->p.rank;
     std::vector<float> h((size_t)S.n * KP);
-    HIPCHK(hipMemcpy(h.data(), S.d_orig.p, h.size() * 4, hipMemcpyDeviceToHost));
+    HIPCHK(copy_st(c, h.data(), S.d_orig.p, h.size() * 4, hipMemcpyDeviceToHost));
     for (int64_t r = 0; r < S.n; ++r) std::memcpy(f_out + (size_t)r * k, &h[(size_t)r * KP], sizeof(float) * k);
   }
   return ALS_OK;
@@ -1546,7 +1562,7 @@ int als_model_create(int32_t rank, int64_t nu, const int32_t* uids, const float*
       std::memcpy(&h[(size_t)r * c->KP], fs[side] + (size_t)ord[r] * rank, sizeof(float) * rank);
     }
     if (S.d_orig.ensure(h.size() * 4) != hipSuccess ||
-        hipMemcpy(S.d_orig.p, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        copy_st(c, S.d_orig.p, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
       als_destroy(c);
       return fail(ALS_E_OUT_OF_MEMORY, "failed to upload factors");
     }
@@ -1718,8 +1734,8 @@ int topk_finish(als_ctx* c, TopkPlan& P) {
   const int64_t np = (int64_t)P.passes.size();
   std::vector<unsigned long long> scanned((size_t)std::max<int64_t>(np, 1), 0ull);
   int cnt[4] = {0, 0, 0, 0};
-  if (np > 0) HIPCHK(hipMemcpy(scanned.data(), P.d_scan.p, np * 8, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(cnt, P.d_cnt.p, 16, hipMemcpyDeviceToHost));
+  if (np > 0) HIPCHK(copy_st(c, scanned.data(), P.d_scan.p, np * 8, hipMemcpyDeviceToHost));
+  HIPCHK(copy_st(c, cnt, P.d_cnt.p, 16, hipMemcpyDeviceToHost));
   for (int64_t q = 0; q < np; ++q) {
     const TopkPlan::PassRec& R = P.passes[q];
     const hipEvent_t* e = P.evs.data() + R.e0;
@@ -2225,12 +2241,12 @@ int als_predict(als_ctx* c, int64_t n, const int32_t* user, const int32_t* item,
   HIPCHK(du.ensure(n * 4));
   HIPCHK(dv.ensure(n * 4));
   HIPCHK(dout.ensure(n * 4));
-  HIPCHK(hipMemcpy(du.p, u.data(), n * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(dv.p, v.data(), n * 4, hipMemcpyHostToDevice));
+  HIPCHK(copy_st(c, du.p, u.data(), n * 4, hipMemcpyHostToDevice));
+  HIPCHK(copy_st(c, dv.p, v.data(), n * 4, hipMemcpyHostToDevice));
   HIPCHK(launch_predict(c->KP, c->p.rank, c->s[ALS_USER].d_orig.as<float>(), c->s[ALS_ITEM].d_orig.as<float>(),
                         du.as<int32_t>(), dv.as<int32_t>(), dout.as<float>(), n, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
-  HIPCHK(hipMemcpy(out, dout.p, n * 4, hipMemcpyDeviceToHost));
+  HIPCHK(copy_st(c, out, dout.p, n * 4, hipMemcpyDeviceToHost));
   return ALS_OK;
 }
 
@@ -2245,14 +2261,14 @@ int als_get_row_ratings(als_ctx* c, int side, int32_t id, int64_t cap, int32_t* 
   if (r < 0) return fail(ALS_E_INVALID_ARGUMENT, "unknown id " + std::to_string(id));
   if (r < S.own0 || r >= S.own0 + S.own_n) return fail(ALS_E_STATE, "row not owned by this rank");
   int64_t pr[2];
-  HIPCHK(hipMemcpy(pr, S.d_ptr.as<int64_t>() + (r - S.own0), 16, hipMemcpyDeviceToHost));
+  HIPCHK(copy_st(c, pr, S.d_ptr.as<int64_t>() + (r - S.own0), 16, hipMemcpyDeviceToHost));
   const int64_t n = pr[1] - pr[0];
   *n_out = n;
   if (n > cap) return ALS_OK;
   std::vector<int32_t> col(n);
   if (n) {
-    HIPCHK(hipMemcpy(col.data(), S.d_col.as<int32_t>() + pr[0], n * 4, hipMemcpyDeviceToHost));
-    if (ratings) HIPCHK(hipMemcpy(ratings, S.d_val.as<float>() + pr[0], n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(copy_st(c, col.data(), S.d_col.as<int32_t>() + pr[0], n * 4, hipMemcpyDeviceToHost));
+    if (ratings) HIPCHK(copy_st(c, ratings, S.d_val.as<float>() + pr[0], n * 4, hipMemcpyDeviceToHost));
   }
   if (src_ids)
     for (int64_t e = 0; e < n; ++e) {
@@ -2310,7 +2326,7 @@ int als_topk_last_rescan(const als_ctx* c, int32_t* src_ids_out, int64_t cap, in
     std::vector<int32_t> need((size_t)c->last_need_n);
     if (c->last_need_n > 0) {
       HIPCHK(hipStreamSynchronize(c->st));
-      HIPCHK(hipMemcpy(need.data(), c->d_last_need.p, need.size() * 4, hipMemcpyDeviceToHost));
+      HIPCHK(copy_st(c, need.data(), c->d_last_need.p, need.size() * 4, hipMemcpyDeviceToHost));
     }
     const Side& S = c->s[c->last_src];
     c->last_rescan.clear();
@@ -2374,9 +2390,9 @@ int als_set_ratings_synthetic(als_ctx* c, uint64_t seed, int32_t rounds, int64_t
   HIPCHK(du.ensure(n * 4));
   HIPCHK(di.ensure(n * 4));
   HIPCHK(dr.ensure(n * 4));
-  HIPCHK(hipMemcpy(dp.p, deg_prefix, (n_users + 1) * 8, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(dcw.p, cw, n_items * 8, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(dperm.p, perm, n_items * 4, hipMemcpyHostToDevice));
+  HIPCHK(copy_st(c, dp.p, deg_prefix, (n_users + 1) * 8, hipMemcpyHostToDevice));
+  HIPCHK(copy_st(c, dcw.p, cw, n_items * 8, hipMemcpyHostToDevice));
+  HIPCHK(copy_st(c, dperm.p, perm, n_items * 4, hipMemcpyHostToDevice));
   int64_t nout = 0;
   HIPCHK(synth_fill(seed, rounds, n_users, n_items, dp.as<int64_t>(), dcw.as<double>(), dperm.as<int32_t>(),
                     du.as<int32_t>(), di.as<int32_t>(), dr.as<float>(), n, &nout, c->st));

@@ -183,7 +183,12 @@ __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB,
     constexpr int cend = (PAIR && c < 8) ? 8 : 16;  // PAIR: the other block's rows are untouched
     if constexpr (!l16_live_ct<PAIR, DM>(c)) return;
     if (!live(c)) return;
-    const float piv = bc16_after_asm<c>(kr[c]);
+    // compiler-scheduled DPP broadcasts (bc16), not the asm helpers of device_common.h: with the asm
+    // row_newbcast FMAs this kernel gave wrong results for a few paired rows from one run to the
+    // next (tools/determinism.py: ~150 of 600K degree <= 8 rows at c2, always the second row of a
+    // unit, 5-55 % off, each time a different set; the ISA scan finds no VALU-to-DPP read inside
+    // two wait states), while the compiler-scheduled form is bit-identical across 20 half-sweeps
+    const float piv = bc16<c>(kr[c]);
     if (!(piv > 0.f)) notpd = true;
     const float inv = frsq(piv), s = piv * inv;
     kr[c] = (i16 == c) ? s : kr[c] * inv;
@@ -192,7 +197,7 @@ __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB,
       constexpr int m = decltype(mm)::value;
       if constexpr (!l16_live_ct<PAIR, DM>(m)) return;
       if (!live(m)) return;
-      fnmac_bc16<m, m == c + 1>(kr[m], kr[c], kr[c]);
+      kr[m] = fmaf(-bc16<m>(kr[c]), kr[c], kr[m]);
     });
     const float yc = bc16<c>(y * dg);
     y = (i16 > c) ? fmaf(-kr[c], yc, y) : ((i16 == c) ? yc : y);

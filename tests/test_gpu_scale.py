@@ -146,6 +146,23 @@ def test_c2_scale_rows_match_fp64_solve(gpu_lib, c2_ctx):
 
 
 @pytest.mark.timeout(400)
+def test_c2_two_contexts_bit_identical(gpu_lib):
+    """Run-to-run identity at BASELINE config 2 (1M users x 200k repos, 50M stars, rank 64): two
+    contexts ingest the same synthetic ratings and run the same item and user half-sweeps side by
+    side; every factor is bit-identical.  (r05: the paired light16 rows -- 600K users of degree <= 8
+    here -- gave ~150 rows 5-55 % off in one context or the other, a different set each run; see
+    tools/determinism.py.)"""
+    a = _ingest(gpu_lib, "c2", 64)
+    b = _ingest(gpu_lib, "c2", 64)
+    for side in (1, 0, 1, 0):
+        a.half(side)
+        b.half(side)
+        fa, fb = a.factors(side)[1], b.factors(side)[1]
+        bad = np.nonzero(np.any(fa.view(np.uint32) != fb.view(np.uint32), axis=1))[0]
+        assert bad.size == 0, f"side {side}: {bad.size} rows differ between two identical runs, e.g. row {bad[0]}"
+
+
+@pytest.mark.timeout(400)
 def test_c3_topk_all_users_after_10_sweeps(gpu_lib, c2_ctx):
     """BASELINE config 3: the c2 fit at 10 sweeps (this module's previous test ran the first), then
     recommendForAllUsers(30) over all 1M users: 2,000 sampled users plus every exact-rescan user are

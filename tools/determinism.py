@@ -46,6 +46,7 @@ def main():
     rep["halves"] = []
     for h in range(args.halves):
         side = 1 if h % 2 == 0 else 0  # item half first (Spark's order)
+        prev = a.factors(side)[1]  # the rows' factors before this half (identical in a and b so far)
         a.half(side)
         b.half(side)
         fa, fb = a.factors(side)[1], b.factors(side)[1]
@@ -60,6 +61,44 @@ def main():
                        degree_hist={"<=8": int((dd <= 8).sum()), "9-16": int(((dd > 8) & (dd <= 16)).sum()),
                                     "17-64": int(((dd > 16) & (dd <= 64)).sum()), ">64": int((dd > 64).sum())},
                        max_rel=float(rel.max()))
+        if n:  # which context is wrong: both against the fp64 solve of Spark's normal equation
+            from tests.test_gpu_parity import _gram_fp64
+            src_side = 1 - side
+            sids, Y = a.factors(src_side)
+            ids = a.factors(side)[0]
+            G = _gram_fp64(Y)
+            errs = []
+            n_row = np.empty(1, np.int64)
+            for r in rows[:20]:
+                rid = int(ids[r])
+                L.check(lib.als_get_row_ratings(a.h, side, rid, 0, None, None, L.ptr(n_row, C.c_int64)))
+                cap = int(n_row[0])
+                src = np.empty(max(cap, 1), np.int32)
+                rat = np.empty(max(cap, 1), np.float32)
+                L.check(lib.als_get_row_ratings(a.h, side, rid, cap, L.ptr(src, C.c_int32), L.ptr(rat, C.c_float),
+                                                L.ptr(n_row, C.c_int64)))
+                m = int(n_row[0])
+                Yr = Y[np.searchsorted(sids, src[:m])].astype(np.float64)
+                cv = 40.0 * np.abs(rat[:m].astype(np.float64))
+                A = G + (Yr.T * cv) @ Yr + 0.5 * np.sum(rat[:m] > 0) * np.eye(args.rank)
+                x = np.linalg.solve(A, Yr.T @ np.where(rat[:m] > 0, 1.0 + cv, 0.0))
+                sc = np.max(np.abs(x))
+                errs.append([float(np.max(np.abs(fa[r] - x)) / sc), float(np.max(np.abs(fb[r] - x)) / sc)])
+            rec["err_vs_fp64_a_b"] = errs
+            # the wrong context's row: its value before the half (never solved), or something else?
+            wrong_is_prev = []
+            for r, (ea, eb) in zip(rows[:20], errs):
+                w = fa[r] if ea > eb else fb[r]
+                wrong_is_prev.append(bool(np.array_equal(w.view(np.uint32), prev[r].view(np.uint32))))
+            rec["wrong_equals_previous"] = wrong_is_prev
+            # light16 pairs: the degree <= 8 rows of the <= 16 bucket in row order, two per unit
+            p8 = np.nonzero(deg[side] <= 8)[0]
+            posn = np.searchsorted(p8, rows[:20])
+            rec["pair_pos"] = posn.tolist()
+            rec["partner_differs"] = [bool(diff[p8[q ^ 1]]) if (q ^ 1) < p8.size else None for q in posn]
+            rec["n_p8"] = int(p8.size)
+            # position of the differing rows in the engine's pair list is not exported; their ids
+            rec["first_ids"] = [int(ids[r]) for r in rows[:20]]
         rep["halves"].append(rec)
         print(json.dumps(rec), flush=True)
         if n:

@@ -14,7 +14,7 @@ for s in "$@"; do
     tests_quick) timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "half_sweep or golden or facade or albedo_protocol" > gpurun_out/tests_quick.log 2>&1 ;;
     tests_topk) timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_recommenders.py -k "topk or ndcg or recommend or transform or facade or albedo" > gpurun_out/tests_topk.log 2>&1 ;;
     tests_scale) timeout -k 10 900 $PYT tests/test_gpu_scale.py -s > gpurun_out/tests_scale.log 2>&1 ;;
-    tests_c3) timeout -k 10 600 $PYT tests/test_gpu_scale.py -s -k "c2_scale or c3" > gpurun_out/tests_c3.log 2>&1 ;;
+    tests_c3) timeout -k 10 600 $PYT tests/test_gpu_scale.py -s -k "c2_scale or c3 or two_contexts" > gpurun_out/tests_c3.log 2>&1 ;;
     tests_all) timeout -k 10 1100 $PYT tests -m gpu > gpurun_out/tests_all.log 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke.log 2>&1 ;;
     bench_c4) timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_c4.json 2> gpurun_out/bench_c4.err ;;
@@ -30,6 +30,8 @@ for s in "$@"; do
     multi) # back-to-back processes on one box (each a fresh context on memory the previous one freed)
       for i in 1 2 3 4 5 6; do timeout -k 10 200 python -u bench.py --steps 2 --warmup 40 --no-cpu --topk-users 0 > gpurun_out/multi_$i.json 2> gpurun_out/multi_$i.err || { echo "multi run $i failed"; exit 1; }; done ;;
     det_c2) timeout -k 10 300 python -u tools/determinism.py --config c2 --rank 64 --halves 20 --out gpurun_out/det_c2.json > gpurun_out/det_c2.log 2>&1 ;;
+    det_c2np) ALBEDO_L16_NOPAIR=1 timeout -k 10 300 python -u tools/determinism.py --config c2 --rank 64 --halves 20 --out gpurun_out/det_c2np.json > gpurun_out/det_c2np.log 2>&1 ;;
+    det_c2ab_*) n=${s#det_c2ab_}; ALBEDO_ALS_LIB=$PWD/tools/ab/$n.so timeout -k 10 300 python -u tools/determinism.py --config c2 --rank 64 --halves 20 --out gpurun_out/$s.json > gpurun_out/$s.log 2>&1 ;;
     det_c4) timeout -k 10 400 python -u tools/determinism.py --config c4 --rank 128 --halves 12 --out gpurun_out/det_c4.json > gpurun_out/det_c4.log 2>&1 ;;
     stress) timeout -k 10 300 python -u bench.py --steps 5 --warmup 300 --no-cpu --topk-users 0 > gpurun_out/stress.json 2> gpurun_out/stress.err ;;
     prof_c5) timeout -k 10 900 tools/prof.sh c5 r03 0 > gpurun_out/prof_c5.log 2>&1 ;;
