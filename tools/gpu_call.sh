@@ -17,6 +17,7 @@ for s in "$@"; do
     tests_c3) timeout -k 10 600 $PYT tests/test_gpu_scale.py -s -k "c2_scale or c3 or two_contexts" > gpurun_out/tests_c3.log 2>&1 ;;
     tests_all) timeout -k 10 1100 $PYT tests -m gpu > gpurun_out/tests_all.log 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke.log 2>&1 ;;
+    bench_default) timeout -k 10 900 python -u bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err ;;
     bench_c4) timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_c4.json 2> gpurun_out/bench_c4.err ;;
     bench_c2) timeout -k 10 300 python -u bench.py --config c2 --steps 10 --warmup 5 > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.err ;;
     bench_c5cpu) timeout -k 10 600 python -u bench.py --config c5 --steps 2 --warmup 1 --topk-users 0 > gpurun_out/bench_c5cpu.json 2> gpurun_out/bench_c5cpu.err ;;
