@@ -623,7 +623,16 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
     s2[h] = __uint_as_float(v.x);
     i2[h] = (int)v.y;
   }
-  wave_bitonic<NS>(s2, i2);
+  // a list of at most 64 entries sorts in one register (the same order: the padding sorts last)
+  if (cnt <= 64) {
+    float s1[1] = {s2[0]};
+    int i1[1] = {i2[0]};
+    wave_bitonic<1>(s1, i1);
+    s2[0] = s1[0];
+    i2[0] = i1[0];
+  } else {
+    wave_bitonic<NS>(s2, i2);
+  }
   const float t = rdlane(s2[0], a.kt - 1);  // the kt-th approximate score (-inf when fewer)
   // Only the best kt candidates are rescored when the list can be certified (n_dst > TOPK_KC): a
   // candidate ranked below kt has approx <= t, so its F2J score is <= t + e, and a certified row has
@@ -633,9 +642,17 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
   const bool rescore = a.n_dst <= TOPK_KC || lane < a.kt;
   const int row = (i2[0] >= 0 && rescore) ? a.perm[i2[0]] : -1;
   const float ex = f2j_dot_rows<KP>(s, a.T, row, a.kreal, s_stage[wave]);
-  double nn = 0.0;
-  for (int c = lane; c < a.kreal; c += 64) nn += (double)s[c] * (double)s[c];
-  for (int o = 32; o > 0; o >>= 1) nn += __shfl_xor(nn, o);
+  // ‖s‖ for the certification bound: the order kernel's value rounded up (a larger ‖s‖ only widens
+  // the bound), else computed here
+  double nsr = 0.0;
+  if (a.sfeat) {
+    nsr = (double)a.sfeat[si * TOPK_SF + TOPK_M + 2];
+  } else {
+    double nn = 0.0;
+    for (int c = lane; c < a.kreal; c += 64) nn += (double)s[c] * (double)s[c];
+    for (int o = 32; o > 0; o >>= 1) nn += __shfl_xor(nn, o);
+    nsr = sqrt(nn);
+  }
   float sc1[1] = {ex};
   int ix1[1] = {row};
   wave_bitonic<1>(sc1, ix1);
@@ -649,7 +666,7 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
     const double kk = (double)(KP + 2);
     const double gam = kk * u / (1.0 - kk * u);
     const double rel = (9.765625e-04 + 2.384185791015625e-07 + 6.0 * gam) * (1.0 + 1.0 / 512.0);
-    const double ns = sqrt(nn), tm = (double)a.tmax_norm;
+    const double ns = nsr, tm = (double)a.tmax_norm;
     const double absu = 2.98023223876953125e-08 * 1.001 * sqrt((double)KP) *
                         (ns / (double)a.tsc + tm / (double)a.ssc) + (double)KP * 8.9e-16 * (double)a.unscale;
     const double e = rel * ns * tm + absu;
