@@ -1641,7 +1641,13 @@ int topk_dst_basis(als_ctx* c, const Side& T, TopkPlan& P, std::vector<double>& 
 // between the k-th exact score and the kt-th approximate one (~1e-3 relative), and k + 16 leaves one
 // while the threshold rises faster than at 64 (fewer dst chunks scanned once the factors converge).
 // The lists still hold 64 and the best 64 are rescored.
-int topk_threshold_rank(int k) { return std::max(k, std::min(TOPK_KC, k + 16)); }
+int topk_threshold_rank(int k) {
+  static const int extra = [] {  // A/B knob
+    const char* e = std::getenv("ALBEDO_TOPK_KTX");
+    return e && *e ? std::max(0, std::atoi(e)) : 16;
+  }();
+  return std::max(k, std::min(TOPK_KC, k + extra));
+}
 
 int topk_plan(als_ctx* c, int src, int k, TopkPlan& P) {
   P.src = src;

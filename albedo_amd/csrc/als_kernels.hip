@@ -479,53 +479,29 @@ __global__ __launch_bounds__(64 * RBF_WAVES) void rotate_bf_kernel(const float* 
   // then sw·cs per column (a global load in the loop would make its vmcnt wait cover the prefetch)
   float* tsc = reinterpret_cast<float*>(sPf + KP * KP * 3) + wave * 16 * RBF_TS;
   float* scs = reinterpret_cast<float*>(sPf + KP * KP * 3) + RBF_WAVES * 16 * RBF_TS;
-  // The next tile's X rows are loaded while this one is on MFMA.  The loads are issued from asm so
-  // that the compiler does not track them: its own wait for them at the loop head would be
-  // vmcnt(0), which also waits for every store of the tile in between (GFX9 counts stores in
-  // vmcnt).  xwait() waits for exactly the loads, leaving the tile's stores (NST per tile) in flight.
+  // The next tile's X rows are loaded while this one is on MFMA, as ordinary loads: the compiler
+  // places the wait for them.  (r03-r05 issued them from asm with a hand-counted vmcnt at the loop
+  // head, leaving the tile's stores in flight; but the compiler, which took the asm results as
+  // ready, copied the loop-carried registers at the loop head before that wait, and a load still in
+  // flight there left a 16-row tile of garbage in Z -- the rare all-paths non-positive pivot of
+  // profiles/r05_bench_c4_notpd_twice_diag.err, src Z max 7e34 from finite src X.)
   auto xload = [&](int64_t t, f32x4 (&xv)[NK][2]) {
     const int64_t row = 16 * t + i16;
     const float* src = X + (row < n ? row : n - 1) * KP + 8 * q;  // unconditional, zeroed past n
 #pragma unroll
     for (int kc = 0; kc < NK; ++kc) {
-      const float* p = src + 32 * kc;
-      f32x4 v0, v1;
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v0) : "v"(p) : "memory");
-      asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "=v"(v1) : "v"(p) : "memory");
-      xv[kc][0] = v0;
-      xv[kc][1] = v1;
-    }
-  };
-  // The counts are checked on the emitted ISA at build time (tools/check_rotate_isa.py, Makefile):
-  // when the check fails the object is rebuilt with ALBEDO_ROTATE_VMCNT0 (every wait drains).
-  auto xwait = [&](f32x4 (&xv)[NK][2], bool after_stores) {
-#ifdef ALBEDO_ROTATE_VMCNT0
-    (void)after_stores;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
-    if (after_stores && Zhl) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // 3 stores per J
-    else if (after_stores) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // 1 store per J
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-#pragma unroll
-    for (int kc = 0; kc < NK; ++kc) {  // the registers are read only after the wait
-      f32x4 v0 = xv[kc][0], v1 = xv[kc][1];
-      asm volatile("" : "+v"(v0), "+v"(v1));
-      xv[kc][0] = v0;
-      xv[kc][1] = v1;
+      xv[kc][0] = ld4(src + 32 * kc);
+      xv[kc][1] = ld4(src + 32 * kc + 4);
     }
   };
   const int64_t tstep = (int64_t)gridDim.x * RBF_WAVES;
   int64_t t = (int64_t)blockIdx.x * RBF_WAVES + wave;
   f32x4 xn[NK][2];
   if (t < ntile) xload(t, xn);
-  bool after_stores = false;
   for (; t < ntile; t += tstep) {
     const int64_t r0 = 16 * t;
     // A operand: row r0 + i16, columns 32kc + 8q .. +7, split into three bf16 parts
     bf16x8 ah[NK], am[NK], al[NK];
-    xwait(xn, after_stores && r0 - 16 * tstep + 15 < n);  // (a ragged last tile stores fewer)
-    after_stores = true;
     {
       const bool in = r0 + i16 < n;
 #pragma unroll

@@ -59,6 +59,7 @@ for s in "$@"; do
     bench_topk_tr) ALBEDO_TOPK_TRACE=1 timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk_tr.json 2> gpurun_out/bench_topk_tr.err ;;
     bench_topk_p*) ALBEDO_TOPK_PASS=${s#bench_topk_p} timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
     bench_topk_d*) ALBEDO_TOPK_DIRSPLIT=${s#bench_topk_d} timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
+    bench_topk_kt*) ALBEDO_TOPK_KTX=${s#bench_topk_kt} timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
     bench_topk) timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk.json 2> gpurun_out/bench_topk.err ;;
     bench_c4q) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 > gpurun_out/bench_c4q.json 2> gpurun_out/bench_c4q.err ;;
     bench_c4q_l*) timeout -k 10 400 python -u bench.py --steps 3 --warmup 5 --no-cpu --topk-users 0 --light ${s#bench_c4q_l} > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
