@@ -1775,18 +1775,18 @@ __device__ void nnls_reg_iterate(const SolveArgs& a, float* smem, int j, int ite
   const int vrow = i16 * NB + R::JB * js;  // this lane's product columns in sG
   const int vown = nnls_vidx(c_own, NB);
   // A·v over the lane's columns, summed over the 16-lane row: the partial of row c_own
+  // (each pair folds into h[s] as soon as it is done: 8 live floats instead of 16 + 8, so the loop
+  // keeps all of A in registers -- no scratch traffic; measured time-neutral)
   auto product = [&](const f32x4 v) -> float {
-    f2 p[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      p[s] = av[s][0] * f2{v[0], v[0]};
-      p[s] = av[s][1] * f2{v[1], v[1]} + p[s];
-      p[s] = av[s][2] * f2{v[2], v[2]} + p[s];
-      p[s] = av[s][3] * f2{v[3], v[3]} + p[s];
-    }
     float h[8];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) h[s] = p[s][0] + dppf<0x140>(p[s][1]);  // row_mirror: lane i^15
+    for (int s = 0; s < 8; ++s) {
+      f2 p = av[s][0] * f2{v[0], v[0]};
+      p = av[s][1] * f2{v[1], v[1]} + p;
+      p = av[s][2] * f2{v[2], v[2]} + p;
+      p = av[s][3] * f2{v[3], v[3]} + p;
+      h[s] = p[0] + dppf<0x140>(p[1]);  // row_mirror: lane i^15
+    }
 #pragma unroll
     for (int s = 0; s < 4; ++s) h[s] += dppf<0x141>(h[s + 4]);  // row_half_mirror: lane i^7
 #pragma unroll
