@@ -749,22 +749,35 @@ __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_
       u[J][r] = (bb & 0x80000000u) ? ~bb : (bb | 0x80000000u);
     }
   }
-  // exact kt-th largest per row: bisection on the key (count of keys >= mid over the row's 16 lanes)
-  float vs[4];
+  // exact kt-th largest per row: bisection on the key (count of keys >= mid over the row's 16 lanes).
+  // The four rows' searches interleave, and each 16-lane count is a DPP butterfly (row_mirror,
+  // row_half_mirror, quad reversal, quad swap: every lane ends with the row's total) -- a __shfl_xor
+  // step is an LDS permute, and 4 x 32 x 4 of them in dependent chains made this kernel ~19 ms at
+  // 20M rows.  Integer counts: the same keys as before.
+  auto row_count = [](int c) {
+    c += __builtin_amdgcn_mov_dpp(c, 0x140, 0xF, 0xF, false);  // row_mirror: lane i^15
+    c += __builtin_amdgcn_mov_dpp(c, 0x141, 0xF, 0xF, false);  // row_half_mirror: lane i^7
+    c += __builtin_amdgcn_mov_dpp(c, 0x1B, 0xF, 0xF, false);   // quad_perm [3,2,1,0]: lane i^3
+    c += __builtin_amdgcn_mov_dpp(c, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]: lane i^1
+    return c;
+  };
+  uint32_t lo[4] = {0u, 0u, 0u, 0u};  // count(>= lo) >= kt always holds (256 keys >= 0)
+  uint32_t hi[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+  for (int it = 0; it < 32; ++it) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    uint32_t lo = 0u, hi = 0xffffffffu;  // count(>= lo) >= kt always holds (256 keys >= 0)
-    for (int it = 0; it < 32; ++it) {
-      const uint32_t mid = lo + (uint32_t)(((uint64_t)hi - lo + 1) >> 1);
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t mid = lo[r] + (uint32_t)(((uint64_t)hi[r] - lo[r] + 1) >> 1);
       int cnt = 0;
 #pragma unroll
       for (int J = 0; J < 16; ++J) cnt += u[J][r] >= mid ? 1 : 0;
-      for (int o = 1; o < 16; o <<= 1) cnt += __shfl_xor(cnt, o);
-      if (cnt >= a.kt) lo = mid;
-      else hi = mid - 1u;
+      cnt = row_count(cnt);
+      if (cnt >= a.kt) lo[r] = mid;
+      else hi[r] = mid - 1u;
     }
-    vs[r] = __uint_as_float((lo & 0x80000000u) ? (lo & 0x7fffffffu) : ~lo);
   }
+  float vs[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) vs[r] = __uint_as_float((lo[r] & 0x80000000u) ? (lo[r] & 0x7fffffffu) : ~lo[r]);
   const int rsel = 4 * g + (i16 & 3);  // the row this lane reports in the group (lanes i16 < 4)
   const double nrm2 = __shfl(ss, rsel);
   const double nrm = sqrt(nrm2);
