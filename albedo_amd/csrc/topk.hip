@@ -702,6 +702,11 @@ __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_
                                                              uint32_t* __restrict__ val, float* __restrict__ thr0,
                                                              float* __restrict__ sfo) {
   constexpr int NQ = KP / 32, RB = 2 * KP;
+  // the dst Gram's leading directions in LDS: every lane reads 32 columns x TOPK_M of them (as global
+  // loads those were half of the kernel's vector memory instructions)
+  __shared__ double sVP[TOPK_M * KP];
+  for (int i = threadIdx.x; i < TOPK_M * KP; i += 256) sVP[i] = a.VP[i];
+  __syncthreads();
   const int lane = threadIdx.x & 63, g = lane >> 4, i16 = lane & 15;
   const int64_t sb = (int64_t)blockIdx.x * 64 + (threadIdx.x >> 6) * 16;  // the wave's first position
   const int64_t si = sb + i16;
@@ -719,7 +724,7 @@ __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_
       const int col = 32 * q + 8 * g + e;
       ss += (double)v * (double)v;
 #pragma unroll
-      for (int d = 0; d < TOPK_M; ++d) spd[d] += (double)v * a.VP[d * KP + col];
+      for (int d = 0; d < TOPK_M; ++d) spd[d] += (double)v * sVP[d * KP + col];
       sf[q][e] = (_Float16)(v * a.ssc);
     }
   }
