@@ -142,10 +142,15 @@ def test_half_sweep_ranks_and_paths(gpu_lib, k, light):
     V_ref = O.half_sweep(U0, B.i_ptr, B.i_col, B.i_val, reg=0.5, alpha=40.0)
     _, V = c.factors(1)
     assert _row_rel(V, V_ref) < 1e-4
+    # rows of degree 65..128 named explicitly (the push-through bucket at light = 96, the wave kernel
+    # otherwise): 73-77 items and 38-52 users of these sets
+    mid = lambda ptr: (np.diff(ptr) > 64) & (np.diff(ptr) <= 128)
+    assert mid(B.i_ptr).sum() > 0 and _row_rel(V[mid(B.i_ptr)], V_ref[mid(B.i_ptr)]) < 1e-4
     c.half(0)  # and back: user half-sweep from the GPU's item factors (exercises the basis chain)
     U_ref = O.half_sweep(V, B.u_ptr, B.u_col, B.u_val, reg=0.5, alpha=40.0)
     _, U = c.factors(0)
     assert _row_rel(U, U_ref) < 1e-4
+    assert mid(B.u_ptr).sum() > 0 and _row_rel(U[mid(B.u_ptr)], U_ref[mid(B.u_ptr)]) < 1e-4
 
 
 @pytest.mark.parametrize("k", [64, 128, 256])
