@@ -534,6 +534,11 @@ int ingest_device(als_ctx* c, int64_t n, const int32_t* d_user, const int32_t* d
   if (n <= 0)
     return fail(ALS_E_INVALID_ARGUMENT, "No ratings available from the input dataset (empty ratings).");
   TRYC(set_device(c));
+  // the previous top-k call's rescan flags index the old id tables: drop them before S.ids changes
+  c->last_rescan.clear();
+  c->last_need_n = 0;
+  c->last_rows.clear();
+  c->last_rescan_ready = true;
   hipStream_t st = c->st;
   DevBuf ud, id;
   HIPCHK(ud.ensure(n * 4));
@@ -882,18 +887,20 @@ std::string failure_diag(als_ctx* c, const Side& S, const Side& T, int64_t ns, c
   DevBuf out;
   std::vector<unsigned long long> h((size_t)ni * 3, 0ull);
   for (int i = 0; i < ni; ++i) h[(size_t)i * 3 + 1] = ~0ull;
+  // an early return drains the stream first: the queued upload reads h and the scans write out
+  auto unavailable = [&]() { (void)hipStreamSynchronize(c->st); return std::string(" [diagnostics unavailable]"); };
   if (out.ensure(h.size() * 8) != hipSuccess ||
       hipMemcpyAsync(out.p, h.data(), h.size() * 8, hipMemcpyHostToDevice, c->st) != hipSuccess)
-    return " [diagnostics unavailable]";
+    return unavailable();
   for (int i = 0; i < ni; ++i)
     if (items[i].p && launch_diag_scan(items[i].p, items[i].n, items[i].f16, out.as<unsigned long long>() + 3 * i, c->st) != hipSuccess)
-      return " [diagnostics unavailable]";
+      return unavailable();
   std::vector<float> lam(KP), cs(KP);
   if (hipMemcpyAsync(h.data(), out.p, h.size() * 8, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
       hipMemcpyAsync(lam.data(), c->d_lam.p, KP * 4, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
       hipMemcpyAsync(cs.data(), c->d_cs.p, KP * 4, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
       hipStreamSynchronize(c->st) != hipSuccess)
-    return " [diagnostics unavailable]";
+    return unavailable();
   std::string r = " [";
   char buf[160];
   for (int i = 0; i < ni; ++i) {
@@ -1056,7 +1063,9 @@ int half_sweep(als_ctx* c, int t) {
   HIPCHK(hipMemcpyAsync(&err, c->d_err.p, 4, hipMemcpyDeviceToHost, st));
   if (c->p.implicit_prefs) HIPCHK(hipMemcpyAsync(&sweeps, eig_sweeps(c->d_eig.as<double>(), KP), 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  T.solver[0] = sweeps;  // Cholesky path: the device eigensolver's Jacobi sweeps (als_solver_stats)
+  // Cholesky path: the device eigensolver's Jacobi sweeps (als_solver_stats), decoded like
+  // als_device_eigh (eig.hip stores -(sweeps + 1) when the budget ran out)
+  T.solver[0] = sweeps < 0 ? -sweeps - 1 : sweeps;
   T.solver[1] = T.solver[2] = T.solver[3] = 0;
   T.t[ALS_T_GRAM] = event_ms(ev[0], ev[1]);
   T.t[ALS_T_EIG] = event_ms(ev[1], ev[2]);  // device eigensolver + the new basis
@@ -1709,6 +1718,19 @@ int topk_plan(als_ctx* c, int src, int k, TopkPlan& P) {
   return ALS_OK;
 }
 
+// Src rows per top-k pass: 2^25 (candidate lists 32 GiB of the 288 GB), or what half of the free
+// device memory holds at ~1.5 KiB per src row (the TOPK_CAP-entry candidate list plus the row's
+// features, order keys and output slots), so a smaller GPU or ranks sharing one fall back to more passes
+static int64_t topk_pass_rows(als_ctx* c) {
+  size_t fr = 0, tot = 0;
+  int64_t cap = (int64_t)1 << 25;
+  if (set_device(c) == ALS_OK && hipMemGetInfo(&fr, &tot) == hipSuccess) {
+    const int64_t fit = (int64_t)(fr / 2 / 1536);
+    cap = std::min<int64_t>(cap, std::max<int64_t>((int64_t)1 << 16, fit & ~(int64_t)0xFFFF));
+  }
+  return cap;
+}
+
 // A call's top-k passes: topk_begin (n_rows positions, at most n_passes passes; the rescan flags of
 // position p land in c->d_last_need[p]), topk_run_rows per pass, topk_finish (one synchronisation:
 // timers and counters).
@@ -1964,9 +1986,9 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   // five passes, 260 ms in one; profiles/r05_bench_c4_topk_pass{4M,10M,20M}.json).  The results are
   // finished and copied out in ranges of pass / 8 rows (at most 4M) while the next range computes.
   // ALBEDO_TOPK_PASS (test knob): rows per pass.
-  const int64_t chunk = [] {
+  const int64_t chunk = [&] {
     const char* e = std::getenv("ALBEDO_TOPK_PASS");
-    return e && *e ? std::max<int64_t>(1 << 16, std::atoll(e)) : (int64_t)1 << 25;
+    return e && *e ? std::max<int64_t>(1 << 16, std::atoll(e)) : topk_pass_rows(c);
   }();
   const int64_t range = std::min<int64_t>((int64_t)1 << 22, std::max<int64_t>(chunk / 8, 1 << 16));
   // world > 1 (SURVEY §8(e) "Top-k: shard users"): rank r scores the r-th contiguous slice of the
@@ -2199,7 +2221,7 @@ int als_evaluate_ndcg(als_ctx* c, int32_t k, int64_t n, const int32_t* user, con
   TRYC(topk_plan(c, ALS_USER, k, P));
   const int64_t per_rank = (nr + c->world - 1) / c->world;
   const int64_t lo = std::min<int64_t>(nr, (int64_t)c->rank * per_rank), hi = std::min<int64_t>(nr, lo + per_rank);
-  const int64_t chunk = 1 << 25;  // one pass for any realistic user count (see als_recommend)
+  const int64_t chunk = topk_pass_rows(c);  // one pass for any realistic user count (see als_recommend)
   DevBuf d_oid, d_osc;
   TRYC(topk_begin(c, P, nr, (hi - lo + chunk - 1) / chunk, rows.data()));
   for (int64_t q0 = lo; q0 < hi; q0 += chunk) {
@@ -2332,8 +2354,13 @@ int als_topk_last_rescan(const als_ctx* c, int32_t* src_ids_out, int64_t cap, in
     }
     const Side& S = c->s[c->last_src];
     c->last_rescan.clear();
-    for (int64_t p = 0; p < c->last_need_n; ++p)
-      if (need[p]) c->last_rescan.push_back(S.ids[c->last_rows_dense ? p : c->last_rows[p]]);
+    const int64_t nrow = (int64_t)S.ids.size();
+    for (int64_t p = 0; p < c->last_need_n; ++p) {
+      if (!need[p]) continue;
+      const int64_t r = c->last_rows_dense ? p : (p < (int64_t)c->last_rows.size() ? c->last_rows[p] : -1);
+      if (r < 0 || r >= nrow) return fail(ALS_E_STATE, "top-k rescan flags out of range of the src rows");
+      c->last_rescan.push_back(S.ids[r]);
+    }
     c->last_rescan_ready = true;
   }
   *n_out = (int64_t)c->last_rescan.size();

@@ -629,8 +629,8 @@ hipError_t launch_rotate(int KP, const float* X, const float* M, float* Z, int64
 // Entries with c = 0 (implicit zero ratings) contribute nothing to A or b and are masked out.
 // =============================================================================================
 // LDS floats per wave: D = 16 keeps K and L as packed lower triangles (+ 64: sink); D = 32 / 64 factor
-// in the MFMA accumulators (wave_chol.h) and need its scratch (WCHOL_SCR floats + NB L⁻¹ tiles)
-__host__ __device__ constexpr int light_wave_lds(int D) { return D == 16 ? D * (D + 1) / 2 + 64 : WCHOL_SCR + (D / 16) * 256; }
+// in the MFMA accumulators (wave_chol.h) and need its scratch (wchol_scratch_floats(NB))
+__host__ __device__ constexpr int light_wave_lds(int D) { return D == 16 ? D * (D + 1) / 2 + 64 : wchol_scratch_floats(D / 16); }
 
 // workgroups per CU: D = 32 at KP = 128 keeps its gathered rows in registers (KEEPZ) and spilled 16
 // VGPRs at 4 (128 VGPRs); at 3 (168) it does not, and the user light half is 1.9 ms faster (r04 A/B)

@@ -56,7 +56,7 @@ struct WaveRow {
   static constexpr int LDS_WAVE = (STAGE + 255) & ~255;
   static constexpr int LDS = WAVES * LDS_WAVE + 2 * KP * 4;  // + column scales and inverses
   static_assert(RPI * RB == 1024 && 8 % RPI == 0, "DMA pieces never cross an 8-rating group");
-  static_assert(LDS_WAVE >= 4 * WCHOL_SCR + NQ * 1024, "the stage doubles as the factor's scratch + L⁻¹ store");
+  static_assert(LDS_WAVE >= 4 * wchol_scratch_floats(NQ), "the stage doubles as the factor's scratch");
 };
 
 // LDS byte offset of (rating r of the stage, column c).  Lane i + 16q reads ratings 8q..8q+7 of

@@ -1276,10 +1276,10 @@ hipError_t launch_scan(const TopkArgs& a, hipStream_t s) {
 // scan 649 -> 438 ms against G = 8 at one per CU), smaller while it leaves CUs without two workgroups
 int topk_rows_per_workgroup(int KP, int64_t n_src, int n_cu) {
   int gmax = KP <= 128 ? 8 : 4;
-  static const int gcap = [] {  // ALBEDO_TOPK_GMAX: A/B knob (2, 4 or 8)
-    const char* e = std::getenv("ALBEDO_TOPK_GMAX");
-    return e && *e ? std::atoi(e) : 4;
-  }();
+  // ALBEDO_TOPK_GMAX: A/B knob, read per call like the other knobs; only 2, 4 or 8 are accepted
+  const char* e = std::getenv("ALBEDO_TOPK_GMAX");
+  const int ge = e && *e ? std::atoi(e) : 4;
+  const int gcap = (ge == 2 || ge == 4 || ge == 8) ? ge : 4;
   gmax = std::min(gmax, std::max(2, gcap));
   for (int G = gmax; G > 2; G /= 2)
     if (n_src >= (int64_t)2 * n_cu * 64 * G) return 64 * G;

@@ -8,12 +8,13 @@
 //   b   bacc[A] in lane i + 16q = b[16A + i] (replicated over q)
 //   x   xs[A], same layout as b
 //
-// Right-looking, 16-wide panels: the diagonal tile goes through LDS into the row layout of chol16
-// (DPP broadcasts), its L⁻¹ comes from a 16-step v_fmac_f32_dpp substitution, the panel row is
-// U = L⁻¹·T on f32 MFMA and the trailing tiles are updated with UᵀU on f32 MFMA -- the C/D layout of
+// Right-looking, 16-wide panels: the diagonal tile goes through LDS into a row layout, one 16-step
+// Gaussian elimination with the inverse riding along gives its L⁻¹ (elim16_inverse), the panel row
+// is U = L⁻¹·T on f32 MFMA and the trailing tiles are updated with UᵀU on MFMA -- the C/D layout of
 // one MFMA is the A and B operand layout of the next, so no tile moves and no workgroup barrier is
-// needed.  The right-hand side follows as a VALU column, then a block back substitution with the
-// kept L⁻¹ tiles.  scr: this wave's LDS scratch, WCHOL_SCR floats + NQ·64 f32x4 (L⁻¹ store).
+// needed.  The right-hand side follows as a VALU column behind the trailing MFMAs, then a
+// right-looking block back substitution with the L⁻¹ images.  scr: this wave's LDS scratch,
+// wchol_scratch_floats(NQ) floats.
 // Returns true when a pivot collapsed (not positive definite; wave-uniform).
 #pragma once
 #include "device_common.h"
@@ -54,31 +55,99 @@ __device__ __forceinline__ f16x8 split_hilo4(f32x4 v) {
   return __builtin_bit_cast(f16x8, (u32x4{w[0], w[1], w[2], w[3]}));
 }
 
+// row_c -> row_i update of the elimination below: x -= f · (x of lane C of the 16-lane row), one
+// v_fmac_f32_dpp whose DPP source is the accumulator register itself (lane C's copy of the same
+// entry).  Every VGPR a DPP instruction reads needs two wait states after its last write; the
+// callers order the updates so that the previous write of x is at least two instructions back and
+// f is written before the step's first update, which carries the s_nop (NOP = true).  The build
+// re-checks the emitted code for exactly this rule (tools/isa_hazards.py).
+template <int C, bool NOP>
+__device__ __forceinline__ void elim_upd(float& x, float f) {
+  if constexpr (NOP)
+    asm volatile("s_nop 1\n\tv_fmac_f32_dpp %0, -%0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+                 : "+v"(x) : "v"(f), "n"(C));
+  else
+    asm volatile("v_fmac_f32_dpp %0, -%0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+                 : "+v"(x) : "v"(f), "n"(C));
+}
+
+// Inverse Cholesky factor of a 16x16 SPD tile by Gaussian elimination with the inverse riding
+// along, in one 16-step chain (the Cholesky and the L⁻¹ substitution were two): lane i + 16q holds
+// row i of the tile (rr, replicated over q) and columns 4q..4q+3 of row i of R (ra, starts as the
+// identity).  Step c: row_i -= (rr_i[c] / rr_c[c]) · row_c for every i > c, on rr and on ra.  The
+// pivots are Cholesky's (d_i = L[i][i]²), R is the unit-lower inverse, so L⁻¹ = diag(d)^(-1/2) R:
+// returned in the A-operand layout (lane i + 16q: L⁻¹[i][4q .. 4q+3]).  Step c + 1's pivot
+// broadcast and multiplier are issued right after step c's first update (column c + 1), so their
+// latency hides behind step c's remaining updates.  notpd: a pivot collapsed below 2^-21 of its
+// start value (numerically singular in fp32; wave-uniform).
+__device__ __forceinline__ f32x4 elim16_inverse(float (&rr)[16], int i16, int q, bool& notpd) {
+  float ra[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) ra[s] = (i16 == 4 * q + s) ? 1.f : 0.f;
+  float d0 = 0.f;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) d0 = (i16 == c) ? rr[c] : d0;
+  float dpiv = 1.f, f;
+  {
+    const float p = bc16_after_asm<0>(rr[0]);
+    f = (i16 > 0) ? rr[0] * frcp(p) : 0.f;
+    dpiv = (i16 == 0) ? p : dpiv;
+  }
+  static_for<0, 16>([&](auto CC) {
+    constexpr int c = decltype(CC)::value;
+    float fn = 0.f;
+    if constexpr (c + 1 < 16) {
+      elim_upd<c, true>(rr[c + 1], f);  // column c + 1 first: the next pivot
+      const float p = bc16_after_asm<c + 1>(rr[c + 1]);
+      fn = (i16 > c + 1) ? rr[c + 1] * frcp(p) : 0.f;
+      dpiv = (i16 == c + 1) ? p : dpiv;
+      static_for<c + 2, 16>([&](auto MM) { elim_upd<c, false>(rr[decltype(MM)::value], f); });
+#pragma unroll
+      for (int s = 0; s < 4; ++s) elim_upd<c, false>(ra[s], f);
+    }
+    f = fn;
+  });
+  notpd = __any(!(dpiv > d0 * 4.76837158e-07f));
+  const float sc = frsq(dpiv);
+  return f32x4{ra[0] * sc, ra[1] * sc, ra[2] * sc, ra[3] * sc};
+}
+
+// Sum over each 16-lane row with the result in every lane of the row: DPP quad permutes, then the
+// half-row and row mirrors (each step adds the same two partial sums in every lane: all 16 lanes end
+// bit-identical)
+__device__ __forceinline__ float sum16_all(float x) {
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));   // quad_perm [1,0,3,2]
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));   // quad_perm [2,3,0,1]
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, true));  // row_half_mirror
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xF, 0xF, true));  // row_mirror
+  return x;
+}
+
 // SPLIT: the trailing updates T -= UᵀU run on v_mfma_f32_16x16x32_f16 with U split into fp16 hi + lo
 // (hi·hi + hi·lo + lo·hi in two MFMAs: k-slots 0..3 / 4..7 of a lane carry the same four rows as hi /
 // lo, so the operands come straight from the C/D registers) instead of four f32 MFMAs: 32 instead of
 // 128 matrix-core cycles per tile update.  The caller scales the system so that every U entry is
 // below 2^14 (|U_ij| <= sqrt(A_jj): max diagonal < 2^28), keeping hi and lo in fp16's normal range.
-// scratch layout: 16 x 16 images with a row stride of 20 floats (80 B), so the 16 rows a ds_read_b128
-// lane group reads start on 16 disjoint 4-bank groups (a 64-B stride put rows i and i + 4 on the same
-// banks); the diagonal tile at 0, b / L⁻¹ at WCHOL_IMG, the L⁻¹ store at WCHOL_SCR
-constexpr int WCHOL_RS = 20, WCHOL_IMG = 16 * WCHOL_RS, WCHOL_SCR = 2 * 16 * WCHOL_RS;
+// Scratch (floats): the diagonal tile's row image at 0, then one L⁻¹ image per panel (row-major), then
+// y (16 per panel).  Images have a row stride of 20 floats (80 B): the 16 rows a ds_read_b128 lane
+// group reads start on 16 disjoint 4-bank groups, and the four rows 4g + r the C/D reads of lane
+// group g touch sit 16 banks apart.
+constexpr int WCHOL_RS = 20, WCHOL_IMG = 16 * WCHOL_RS;
+__host__ __device__ constexpr int wchol_scratch_floats(int nq) { return WCHOL_IMG * (nq + 1) + 16 * nq; }
 
 template <int NQ, bool SPLIT = false>
 __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2], float (&bacc)[NQ], float* scr,
                                                 float (&xs)[NQ]) {
   const int lane = threadIdx.x & 63, q = lane >> 4, i16 = lane & 15;
-  // L⁻¹ of every panel in the A-operand layout (lane i + 16q: L⁻¹[i][4q .. 4q+3]), kept in the dead
-  // stage for the back substitution: [NQ][64 lanes] f32x4 after the two scratch tiles
-  f32x4* s_linv = reinterpret_cast<f32x4*>(scr + WCHOL_SCR);
+  float* s_y = scr + WCHOL_IMG * (NQ + 1);  // y of every panel in the lane-group layout
   bool notpd = false;
   WCHOL_T0();
   static_for<0, NQ>([&](auto JB) {
     constexpr int jb = decltype(JB)::value, td = tix(jb, jb, NQ);
-    // diagonal tile to the row layout of chol16 (lane i: row i, replicated over the 4 lane groups)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) scr[(4 * q + r) * WCHOL_RS + i16] = acc[td][r];
-    if (q == 0) scr[WCHOL_IMG + i16] = bacc[jb];  // b_jb alongside (the L⁻¹ image overwrites it later)
+    float* img = scr + WCHOL_IMG * (jb + 1);  // this panel's L⁻¹, row-major
+    // diagonal tile to the row layout of the elimination: lane i + 16q holds (D[4q + r][i])_r =
+    // row i, columns 4q .. 4q+3 of the (symmetric) tile -- one b128 store per lane; lane i reads row i
+    *reinterpret_cast<f32x4*>(scr + WCHOL_RS * i16 + 4 * q) = acc[td];
     WAVE_LDS_SYNC();
     float rr[16];
 #pragma unroll
@@ -87,40 +156,13 @@ __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2],
 #pragma unroll
       for (int e = 0; e < 4; ++e) rr[4 * u + e] = v[e];
     }
-    const f32x4 bt = ld4(scr + WCHOL_IMG + 4 * q);  // lane i + 16q: b_jb[4q .. 4q+3] (the MFMA k layout)
-    float dg = 1.f;
     WCHOL_PH(0);
-    notpd |= chol16(rr, dg, i16);
+    bool np;
+    const f32x4 lv = elim16_inverse(rr, i16, q, np);  // lane i + 16q: L⁻¹[i][4q .. 4q+3]
+    notpd |= np;
     WCHOL_PH(1);
-    // chol16 ends in inline asm: two wait states before any DPP read of its results
-    asm volatile("s_nop 1"
-                 : "+v"(rr[0]), "+v"(rr[1]), "+v"(rr[2]), "+v"(rr[3]), "+v"(rr[4]), "+v"(rr[5]), "+v"(rr[6]),
-                   "+v"(rr[7]), "+v"(rr[8]), "+v"(rr[9]), "+v"(rr[10]), "+v"(rr[11]), "+v"(rr[12]),
-                   "+v"(rr[13]), "+v"(rr[14]), "+v"(rr[15]), "+v"(dg));
-    // column i16 of L⁻¹: L x = e_i16 by forward substitution, L[r][m] broadcast from lane r.  Right-
-    // looking (x_m, then every later row's update by x_m): the updates of one step are independent, so
-    // the dependent chain is 16 steps long instead of 120 FMAs; each row still accumulates its terms
-    // in increasing m (the same roundings as the dot-product order).
-    float x[16];  // row r's running value until step r, then L⁻¹[r][i16]
-#pragma unroll
-    for (int r = 0; r < 16; ++r) x[r] = (i16 == r) ? 1.f : 0.f;
-    static_for<0, 16>([&](auto MM) {
-      constexpr int m = decltype(MM)::value;
-      x[m] *= bc16_after_asm<m>(dg);
-      // one v_fmac_f32_dpp per term (asm keeps the broadcasts from being hoisted into registers)
-      static_for<m + 1, 16>([&](auto RR) {
-        constexpr int r = decltype(RR)::value;
-        fnmac_bc16<r, false>(x[r], rr[m], x[m]);
-      });
-    });
-    if (q == 0) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) scr[WCHOL_IMG + WCHOL_RS * r + i16] = x[r];
-    }
-    WAVE_LDS_SYNC();
-    const f32x4 lv = ld4(scr + WCHOL_IMG + WCHOL_RS * i16 + 4 * q);
-    s_linv[jb * 64 + lane] = lv;
-    WCHOL_PH(2);
+    // L⁻¹ image: the RHS and the back substitution read it in the C/D layout
+    *reinterpret_cast<f32x4*>(img + WCHOL_RS * i16 + 4 * q) = lv;
     // panel row: U(jb, I) = L⁻¹ T(jb, I)  (A = L⁻¹ rows, B = the tile's C/D registers)
     static_for<jb + 1, NQ>([&](auto II) {
       constexpr int I = decltype(II)::value, t = tix(jb, I, NQ);
@@ -129,27 +171,11 @@ __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2],
       for (int s = 0; s < 4; ++s) u = mfma4(lv[s], acc[t][s], u);
       acc[t] = u;
     });
-    // RHS: y_jb = L⁻¹ b_jb, then b_M -= U(jb, M)ᵀ y_jb for the blocks below (VALU + shuffles: the
-    // same products on the f32 MFMA -- 8 + 4 per block -- measured slower, they compete with the
-    // other wave's build for the matrix core)
-    WCHOL_PH(3);
-    float yp = 0.f;
+    // lane c + 16g: L⁻¹[4g + r][c] (the LDS pipe is in order: the image stores above come first)
+    float lc[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) yp = fmaf(lv[s], bt[s], yp);
-    yp = rows4_sum(yp);
-    bacc[jb] = yp;
-    // y[4q .. 4q+3] to lane group q through the scratch (the L⁻¹ image's first row is already read)
-    if (q == 0) scr[WCHOL_IMG + i16] = yp;
-    WAVE_LDS_SYNC();
-    const f32x4 y4 = ld4(scr + WCHOL_IMG + 4 * q);
-    static_for<jb + 1, NQ>([&](auto MM) {
-      constexpr int M = decltype(MM)::value, t = tix(jb, M, NQ);
-      float pv = 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) pv = fmaf(acc[t][r], y4[r], pv);
-      bacc[M] -= rows4_sum(pv);
-    });
-    WCHOL_PH(4);
+    for (int r = 0; r < 4; ++r) lc[r] = img[WCHOL_RS * (4 * q + r) + i16];
+    WCHOL_PH(2);
     // trailing tiles: T(M, I) -= U(jb, M)ᵀ U(jb, I), the next diagonal tile first
     if constexpr (SPLIT) {
       typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -179,35 +205,51 @@ __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2],
         });
       });
     }
-    WAVE_LDS_SYNC();  // scratch reads done before the next panel rewrites it
+    WCHOL_PH(3);
+    // RHS, behind the trailing MFMAs: y_jb = L⁻¹ b_jb straight into the lane-group layout (lane c + 16g:
+    // Σ_c L⁻¹[4g + r][c] b[c] summed over the row, y[4g + r] in every lane of group g), then
+    // b_M -= U(jb, M)ᵀ y_jb for the blocks below (lane c + 16g: Σ_r U[4g + r][c] y[4g + r], summed
+    // over the four groups) -- no LDS round trip on this chain
+    float y4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y4[r] = sum16_all(lc[r] * bacc[jb]);
+    if (i16 == 0) *reinterpret_cast<f32x4*>(s_y + 16 * jb + 4 * q) = f32x4{y4[0], y4[1], y4[2], y4[3]};
+    static_for<jb + 1, NQ>([&](auto MM) {
+      constexpr int M = decltype(MM)::value, t = tix(jb, M, NQ);
+      float pv = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pv = fmaf(acc[t][r], y4[r], pv);
+      bacc[M] -= rows4_sum(pv);
+    });
+    WCHOL_PH(4);
+    WAVE_LDS_SYNC();  // scratch reads done before the next panel rewrites the row image
     WCHOL_PH(5);
   });
 
-  // ---- back substitution: x_jb = L_jb⁻ᵀ (y_jb - Σ_{M > jb} U(jb, M) x_M) ------------------------
+  // ---- back substitution: x_jb = L_jb⁻ᵀ (y_jb - Σ_{M > jb} U(jb, M) x_M), right-looking: as soon as
+  // x_M is known every block above takes its products (lane c + 16g: U(jb, M)[4g + r][c] x_M[c]), so
+  // the chain per block is one row sum, L⁻ᵀ on the lane-group layout and one cross-group sum
+  float pr[NQ][4];
+#pragma unroll
+  for (int b = 0; b < NQ; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pr[b][r] = 0.f;
   static_for<0, NQ>([&](auto KK) {
     constexpr int jb = NQ - 1 - decltype(KK)::value;
-    float pr[4] = {0.f, 0.f, 0.f, 0.f};  // lane c + 16g: Σ_M U(jb, M)[4g + r][c] x_M[c]
-    static_for<jb + 1, NQ>([&](auto MM) {
-      constexpr int M = decltype(MM)::value, t = tix(jb, M, NQ);
+    const float* img = scr + WCHOL_IMG * (jb + 1);
+    const f32x4 yb = ld4(s_y + 16 * jb + 4 * q);  // y[4g .. 4g+3]
+    float xp = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) pr[r] = fmaf(acc[t][r], xs[M], pr[r]);
+    for (int r = 0; r < 4; ++r) {
+      const float t = yb[r] - sum16_all(pr[jb][r]);       // t[4g + r] in every lane of group g
+      xp = fmaf(img[WCHOL_RS * (4 * q + r) + i16], t, xp);  // L⁻¹[4g + r][c] t[4g + r]
+    }
+    xs[jb] = rows4_sum(xp);  // x[c] in lane c of every group
+    static_for<0, jb>([&](auto BB) {
+      constexpr int b = decltype(BB)::value, t = tix(b, jb, NQ);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pr[b][r] = fmaf(acc[t][r], xs[jb], pr[b][r]);
     });
-    float tq[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) tq[r] = sum16_last(pr[r]);  // row 4g + r in lane 15 + 16g
-    // lane i + 16q gets t_i = y_i - (row i's sum): row i lives in lane 15 + 16(i >> 2), slot i & 3,
-    // gathered through the scratch (one store + one load instead of four shuffles)
-    const f32x4 lv = s_linv[jb * 64 + lane];
-    if (i16 == 15) *reinterpret_cast<f32x4*>(scr + 4 * q) = f32x4{tq[0], tq[1], tq[2], tq[3]};
-    WAVE_LDS_SYNC();
-    const float ti = bacc[jb] - scr[i16];
-    // x = L⁻ᵀ t: lane k + 16q holds L⁻¹[k][4q + s]; x[4q + s] = Σ_k L⁻¹[k][4q + s] t_k
-    float xq[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) xq[s] = sum16_last(lv[s] * ti);  // x[4g + s] in lane 15 + 16g
-    if (i16 == 15) *reinterpret_cast<f32x4*>(scr + 16 + 4 * q) = f32x4{xq[0], xq[1], xq[2], xq[3]};
-    WAVE_LDS_SYNC();
-    xs[jb] = scr[16 + i16];
   });
   WCHOL_PH(6);
   WCHOL_OUT();

@@ -54,8 +54,8 @@ for s in "$@"; do
     c1p) timeout -k 10 900 python -u tools/c1p_job.py --out gpurun_out/c1p_job.json > gpurun_out/c1p_job.log 2>&1 ;;
     tests_eig) timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "device_eigensolver or half_sweep_ranks or orthogonal" > gpurun_out/tests_eig.log 2>&1 ;;
     pmc_topk4) timeout -k 10 600 tools/pmc_topk4.sh r04 > gpurun_out/pmc_topk4.log 2>&1 ;;
-    bench_topk_g48) ALBEDO_TOPK_GMAX=48 timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk_g48.json 2> gpurun_out/bench_topk_g48.err ;;
-    tests_topk_g48) ALBEDO_TOPK_GMAX=48 timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_recommenders.py -k "topk or ndcg or recommend or transform or facade or albedo" > gpurun_out/tests_topk_g48.log 2>&1 ;;
+    bench_topk_g8) ALBEDO_TOPK_GMAX=8 timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk_g8.json 2> gpurun_out/bench_topk_g8.err ;;
+    tests_topk_g8) ALBEDO_TOPK_GMAX=8 timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_recommenders.py -k "topk or ndcg or recommend or transform or facade or albedo" > gpurun_out/tests_topk_g8.log 2>&1 ;;
     bench_topk_g4) ALBEDO_TOPK_GMAX=4 timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk_g4.json 2> gpurun_out/bench_topk_g4.err ;;
     topkph_g4) ALBEDO_TOPK_GMAX=4 timeout -k 10 400 python -u tools/topk_phases.py --lib tools/ab/topkph.so --out gpurun_out/topkph_g4.json > gpurun_out/topkph_g4.log 2>&1 ;;
     bench_topk_tr) ALBEDO_TOPK_TRACE=1 timeout -k 10 400 python -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/bench_topk_tr.json 2> gpurun_out/bench_topk_tr.err ;;

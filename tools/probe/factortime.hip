@@ -62,7 +62,7 @@ int main(int argc, char** argv) {
     double pa[8] = {0}; int64_t pn = 0;
     for (int64_t i = 0; i < nrows; i += 7, ++pn)
       for (int q = 0; q < 8; ++q) pa[q] += (double)hph[i * 8 + q];
-    printf("  phases (cycles/row): diag-to-rows %.0f  diag_block %.0f  linv-image %.0f  panel-U %.0f  rhs %.0f  trailing %.0f  back-sub %.0f\n",
+    printf("  phases (cycles/row): diag-to-rows %.0f  elim16 %.0f  image+U %.0f  trailing %.0f  rhs %.0f  sync %.0f  back-sub %.0f\n",
            pa[0] / pn, pa[1] / pn, pa[2] / pn, pa[3] / pn, pa[4] / pn, pa[5] / pn, pa[6] / pn);
     int herr = 0; CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
     printf("waves/SIMD %d: %8.3f ms for %lld rows (%.1f ns/row), factor cycles/row %.0f, err %d\n", occ, ms,
