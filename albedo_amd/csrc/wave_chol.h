@@ -71,45 +71,81 @@ __device__ __forceinline__ void elim_upd(float& x, float f) {
                  : "+v"(x) : "v"(f), "n"(C));
 }
 
+// Lane group G's value of x in every lane (same lane within the 16-lane row): v_permlane16_swap
+// leaves rows (0, 0, 2, 2) in its first result and (1, 1, 3, 3) in its second, v_permlane32_swap of
+// that leaves (0, 1, 0, 1) / (2, 3, 2, 3); G picks the results at compile time, so the broadcast is
+// two VALU instructions and no selects (tools/probe/permlane_probe.hip checks the semantics)
+template <int G>
+__device__ __forceinline__ float grp_bcast(float x) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  const uint32_t p = (G & 1) ? a[1] : a[0];
+  const auto b = __builtin_amdgcn_permlane32_swap(p, p, false, false);
+  return __uint_as_float((G & 2) ? b[1] : b[0]);
+}
+
 // Inverse Cholesky factor of a 16x16 SPD tile by Gaussian elimination with the inverse riding
-// along, in one 16-step chain (the Cholesky and the L⁻¹ substitution were two): lane i + 16q holds
-// row i of the tile (rr, replicated over q) and columns 4q..4q+3 of row i of R (ra, starts as the
-// identity).  Step c: row_i -= (rr_i[c] / rr_c[c]) · row_c for every i > c, on rr and on ra.  The
-// pivots are Cholesky's (d_i = L[i][i]²), R is the unit-lower inverse, so L⁻¹ = diag(d)^(-1/2) R:
-// returned in the A-operand layout (lane i + 16q: L⁻¹[i][4q .. 4q+3]).  Step c + 1's pivot
-// broadcast and multiplier are issued right after step c's first update (column c + 1), so their
-// latency hides behind step c's remaining updates.  notpd: a pivot collapsed below 2^-21 of its
-// start value (numerically singular in fp32; wave-uniform).
-__device__ __forceinline__ f32x4 elim16_inverse(float (&rr)[16], int i16, int q, bool& notpd) {
-  float ra[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) ra[s] = (i16 == 4 * q + s) ? 1.f : 0.f;
+// along, in one 16-step chain, the work spread over the four lane groups.  Row i of the
+// concatenation [X | R] (X the tile, R starting as the identity) has 32 columns, and at step c
+// exactly 16 of them change: X's c+1..15 and R's 0..c.  Lane i + 16q keeps, for each of the four
+// columns m = 4q + s of its group, one register w[s]: X[i][m] until step m, then R[i][m] -- at step
+// m column m of X has served as the pivot column and R's column m starts to change, so every lane
+// updates exactly four live entries per step (the tile, replicated over the groups, took 15 - c
+// updates plus the inverse's).  Step c: the pivot X[c][c] by readlane (uniform), the owner group
+// G = c >> 2 forms the multipliers f_i = X[i][c] / X[c][c] (i > c) from its register, grp_bcast
+// hands them to every group, the owner slot restarts as R's column c (e_c), and each
+// w[s] -= f_i · (w[s] of lane c) -- one v_fmac_f32_dpp whose DPP source is the register itself (the
+// owner slot becomes e_c - f, R's column c after step c).  The pivots are Cholesky's (d_i = L[i][i]²), R is the unit-lower inverse, so
+// L⁻¹ = diag(d)^(-1/2) R, returned in the A-operand layout (lane i + 16q: L⁻¹[i][4q .. 4q+3]).
+// The tile arrives in the MFMA C/D layout (lane i + 16q: D[4q + r][i] = D[i][4q + r] by symmetry),
+// which is already this layout: no LDS round trip.  Step c + 1's pivot and multipliers are formed
+// right after step c updates column c + 1 (its register goes first), so their latency hides behind
+// step c's remaining updates.  notpd: a pivot collapsed below 2^-21 of its start value
+// (numerically singular in fp32; wave-uniform).
+__device__ __forceinline__ f32x4 elim16_inverse(f32x4 tile, int i16, int q, bool& notpd) {
+  float w[4] = {tile[0], tile[1], tile[2], tile[3]};
+  // start diagonal D[i][i] (lane i of group i >> 2, slot i & 3); the check runs in those lanes only
+  const bool own = q == (i16 >> 2);
   float d0 = 0.f;
 #pragma unroll
-  for (int c = 0; c < 16; ++c) d0 = (i16 == c) ? rr[c] : d0;
-  float dpiv = 1.f, f;
-  {
-    const float p = bc16_after_asm<0>(rr[0]);
-    f = (i16 > 0) ? rr[0] * frcp(p) : 0.f;
-    dpiv = (i16 == 0) ? p : dpiv;
-  }
+  for (int s = 0; s < 4; ++s) d0 = (own && (i16 & 3) == s) ? w[s] : d0;
+  float dpiv = 1.f;
+  uint64_t gmask[4];  // lanes of group g (the owner slot's switch to R)
+#pragma unroll
+  for (int g = 0; g < 4; ++g) gmask[g] = __ballot(q == g);
+  float eye[4];  // R's start: lane i + 16q, slot s = (i == 4q + s)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) eye[s] = (i16 == 4 * q + s) ? 1.f : 0.f;
+  // multipliers of step c from the current register of column c (wave-uniform pivot by readlane)
+  auto mult = [&](auto CC) {
+    constexpr int c = decltype(CC)::value, G = c >> 2, S = c & 3;
+    const float p = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w[S]), 16 * G + c));
+    dpiv = (i16 == c) ? p : dpiv;
+    const float fo = (i16 > c) ? w[S] * frcp(p) : 0.f;  // right in group G only
+    return grp_bcast<G>(fo);
+  };
+  float f = mult(std::integral_constant<int, 0>{});
   static_for<0, 16>([&](auto CC) {
-    constexpr int c = decltype(CC)::value;
+    constexpr int c = decltype(CC)::value, G = c >> 2, S = c & 3;
+    // owner slot: X's column c is spent once its multipliers are formed; it restarts as R's column c
+    // (e_c), and the step's own update below makes it e_c - f.  A volatile asm select: left to
+    // itself the compiler sinks it next to the register's update, whose DPP read then follows the
+    // write inside the two wait states (tools/isa_hazards.py); the owner slot's update goes last
+    asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(w[S]) : "v"(eye[S]), "s"(gmask[G]));
     float fn = 0.f;
     if constexpr (c + 1 < 16) {
-      elim_upd<c, true>(rr[c + 1], f);  // column c + 1 first: the next pivot
-      const float p = bc16_after_asm<c + 1>(rr[c + 1]);
-      fn = (i16 > c + 1) ? rr[c + 1] * frcp(p) : 0.f;
-      dpiv = (i16 == c + 1) ? p : dpiv;
-      static_for<c + 2, 16>([&](auto MM) { elim_upd<c, false>(rr[decltype(MM)::value], f); });
-#pragma unroll
-      for (int s = 0; s < 4; ++s) elim_upd<c, false>(ra[s], f);
+      constexpr int SN = (c + 1) & 3;
+      elim_upd<c, true>(w[SN], f);  // column c + 1's register first: the next pivot
+      fn = mult(std::integral_constant<int, c + 1>{});
+      static_for<1, 4>([&](auto KK) {  // SN + 3 = S: the owner slot last
+        constexpr int s = (SN + decltype(KK)::value) & 3;
+        elim_upd<c, false>(w[s], f);
+      });
     }
     f = fn;
   });
-  notpd = __any(!(dpiv > d0 * 4.76837158e-07f));
+  notpd = __any(own && !(dpiv > d0 * 4.76837158e-07f));
   const float sc = frsq(dpiv);
-  return f32x4{ra[0] * sc, ra[1] * sc, ra[2] * sc, ra[3] * sc};
+  return f32x4{w[0] * sc, w[1] * sc, w[2] * sc, w[3] * sc};
 }
 
 // Sum over each 16-lane row with the result in every lane of the row: DPP quad permutes, then the
@@ -145,20 +181,9 @@ __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2],
   static_for<0, NQ>([&](auto JB) {
     constexpr int jb = decltype(JB)::value, td = tix(jb, jb, NQ);
     float* img = scr + WCHOL_IMG * (jb + 1);  // this panel's L⁻¹, row-major
-    // diagonal tile to the row layout of the elimination: lane i + 16q holds (D[4q + r][i])_r =
-    // row i, columns 4q .. 4q+3 of the (symmetric) tile -- one b128 store per lane; lane i reads row i
-    *reinterpret_cast<f32x4*>(scr + WCHOL_RS * i16 + 4 * q) = acc[td];
-    WAVE_LDS_SYNC();
-    float rr[16];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const f32x4 v = ld4(scr + WCHOL_RS * i16 + 4 * u);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) rr[4 * u + e] = v[e];
-    }
     WCHOL_PH(0);
     bool np;
-    const f32x4 lv = elim16_inverse(rr, i16, q, np);  // lane i + 16q: L⁻¹[i][4q .. 4q+3]
+    const f32x4 lv = elim16_inverse(acc[td], i16, q, np);  // lane i + 16q: L⁻¹[i][4q .. 4q+3]
     notpd |= np;
     WCHOL_PH(1);
     // L⁻¹ image: the RHS and the back substitution read it in the C/D layout

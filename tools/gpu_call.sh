@@ -74,6 +74,7 @@ for s in "$@"; do
     debug_eig) timeout -k 10 600 python -u tools/debug_eig.py > gpurun_out/debug_eig.log 2>&1; r=$?; echo "debug_eig rc $r"; [ $r -le 1 ] ;;
     debug_c1) timeout -k 10 300 python -u tools/debug_c1.py > gpurun_out/debug_c1.log 2>&1; r=$?; echo "debug_c1 rc $r"; [ $r -le 1 ] ;;
     protocol_eu) { timeout -k 10 300 python -u tools/protocol_eu.py main; } > gpurun_out/protocol_eu.log 2>&1 ;;
+    permlane) (cd tools/probe && timeout -k 5 60 ./permlane_probe) > gpurun_out/permlane.txt 2>&1 ;;
     factortime)(cd tools/probe && timeout -k 5 120 ./factortime 1000000) > gpurun_out/factortime.txt 2>&1 ;;
     prot_*) n=${s#prot_}; { ALBEDO_ALS_LIB=$PWD/tools/ab/$n.so timeout -k 10 300 python -u tools/protocol_eu.py $n; } > gpurun_out/prot_$n.log 2>&1 ;;
     topkph) timeout -k 10 400 python -u tools/topk_phases.py --lib tools/ab/topkph.so --out gpurun_out/topkph.json > gpurun_out/topkph.log 2>&1 ;;
