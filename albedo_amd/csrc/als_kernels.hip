@@ -457,7 +457,7 @@ __global__ void rotate_pfrag_kernel(const float* __restrict__ P, __bf16* __restr
   Pf[base + 1024] = pl;
 }
 
-constexpr int RBF_WAVES = 8, RBF_TS = 20;  // waves per block, transpose row stride (floats)
+constexpr int RBF_WAVES = 8, RBF_TS = 72;  // waves per block, output image row stride (floats)
 constexpr int RBF_JU = 4;                  // column blocks whose accumulator chains interleave
 template <int KP>
 __global__ __launch_bounds__(64 * RBF_WAVES) void rotate_bf_kernel(const float* __restrict__ X, const __bf16* __restrict__ Pf,
@@ -475,7 +475,7 @@ __global__ __launch_bounds__(64 * RBF_WAVES) void rotate_bf_kernel(const float* 
       reinterpret_cast<float*>(sPf + KP * KP * 3)[RBF_WAVES * 16 * RBF_TS + c] = sw * cs[c];
   __syncthreads();
   const int64_t ntile = (n + 15) / 16;
-  // this wave's output transpose (C layout -> rows of 4 consecutive columns per lane), 20-float rows;
+  // this wave's output image (C layout -> 16 consecutive columns of one row per lane), 72-float rows;
   // then sw·cs per column (a global load in the loop would make its vmcnt wait cover the prefetch)
   float* tsc = reinterpret_cast<float*>(sPf + KP * KP * 3) + wave * 16 * RBF_TS;
   float* scs = reinterpret_cast<float*>(sPf + KP * KP * 3) + RBF_WAVES * 16 * RBF_TS;
@@ -495,10 +495,9 @@ __global__ __launch_bounds__(64 * RBF_WAVES) void rotate_bf_kernel(const float* 
     }
   };
   const int64_t tstep = (int64_t)gridDim.x * RBF_WAVES;
-  int64_t t = (int64_t)blockIdx.x * RBF_WAVES + wave;
-  f32x4 xn[NK][2];
-  if (t < ntile) xload(t, xn);
-  for (; t < ntile; t += tstep) {
+  // one 16-row tile: split the A operand, refill its registers with tile tn (two tiles in flight per
+  // wave: the one this tile's loads were issued with and tn), then the MFMAs and the stores
+  auto tile = [&](int64_t t, f32x4 (&xn)[NK][2], int64_t tn) {
     const int64_t r0 = 16 * t;
     // A operand: row r0 + i16, columns 32kc + 8q .. +7, split into three bf16 parts
     bf16x8 ah[NK], am[NK], al[NK];
@@ -517,12 +516,14 @@ __global__ __launch_bounds__(64 * RBF_WAVES) void rotate_bf_kernel(const float* 
           al[kc][e] = (__bf16)(r1 - (float)m);
         }
     }
-    if (t + tstep < ntile) xload(t + tstep, xn);
-    // output rows: lane l writes row r0 + (l & 15), columns 16J + 4(l >> 4) .. +3
-    const int orow = lane & 15, oc = 4 * (lane >> 4);  // 16 lanes: 16 rows of one 16-B unit (conflict-free reads)
+    if (tn < ntile) xload(tn, xn);
+    // output: per group of RBF_JU = 4 column blocks (64 columns) the accumulators go through this
+    // wave's LDS image [16 rows][RBF_TS], 16-B chunk ch of row r at chunk position ch ^ r (conflict-free
+    // b32 stores and b128 reads); lane l then holds row r0 + (l & 15), columns 16q .. 16q + 15 of the
+    // group and writes them as 16-B stores only -- 4 for Z, 2 + 2 for the fp16 hi / lo split (r05:
+    // 4-column pieces, dwordx2 split stores and two LDS waits per 16 columns)
+    const int orow = lane & 15;
     const int64_t rr = r0 + orow;
-    // RBF_JU column blocks per step: their accumulator chains interleave (each chain keeps its own
-    // product order, so Z is bit-identical to one block at a time)
     for (int J2 = 0; J2 < NJ; J2 += RBF_JU) {
       f32x4 acc2[RBF_JU];
 #pragma unroll
@@ -550,36 +551,54 @@ __global__ __launch_bounds__(64 * RBF_WAVES) void rotate_bf_kernel(const float* 
 #pragma unroll
         for (int u = 0; u < RBF_JU; ++u) acc2[u] = mfma_b(ah[kc], bh[u], acc2[u]);
       }
+      // C layout (lane j + 16q: Z[r0 + 4q + r][16(J2 + u) + j]) -> the image
 #pragma unroll
-     for (int u = 0; u < RBF_JU; ++u) {
-      const int J = J2 + u;
-      const f32x4 acc = acc2[u];
-      // C layout (lane j + 16q: Z[r0 + 4q + r][16J + j]) -> LDS -> 16-B row pieces
+      for (int u = 0; u < RBF_JU; ++u)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) tsc[(4 * q + r) * RBF_TS + i16] = acc[r];
+        for (int r = 0; r < 4; ++r) {
+          const int row = 4 * q + r, ch = 4 * u + (i16 >> 2);
+          tsc[row * RBF_TS + 4 * (ch ^ row) + (i16 & 3)] = acc2[u][r];
+        }
       WAVE_LDS_SYNC();
-      const f32x4 z4 = ld4(tsc + orow * RBF_TS + oc);
+      f32x4 z4[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) z4[k] = ld4(tsc + orow * RBF_TS + 4 * ((4 * q + k) ^ orow));
       WAVE_LDS_SYNC();
-      const int c = 16 * J + oc;
+      const int c0 = 16 * J2 + 16 * q;
       if (rr < n) {
-        *reinterpret_cast<f32x4*>(Z + rr * KP + c) = z4;
-        if (Zhl) {
-          f16x4 h4, l4;
-          const f32x4 cw4 = ld4(scs + c);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float v = z4[e] * cw4[e];
-            asm("" : "+v"(v));  // one fp32 rounding; hi and lo both from that value (presplit_kernel)
-            const _Float16 hv = (_Float16)v;
-            h4[e] = hv;
-            l4[e] = (_Float16)(v - (float)hv);
+        for (int k = 0; k < 4; ++k) *reinterpret_cast<f32x4*>(Z + rr * KP + c0 + 4 * k) = z4[k];
+        if (Zhl) {
+          f16x8 h8[2], l8[2];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const f32x4 cw4 = ld4(scs + c0 + 4 * k);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float v = z4[k][e] * cw4[e];
+              asm("" : "+v"(v));  // one fp32 rounding; hi and lo both from that value (presplit_kernel)
+              const _Float16 hv = (_Float16)v;
+              h8[k >> 1][4 * (k & 1) + e] = hv;
+              l8[k >> 1][4 * (k & 1) + e] = (_Float16)(v - (float)hv);
+            }
           }
-          *reinterpret_cast<f16x4*>(Zhl + rr * 2 * KP + c) = h4;
-          *reinterpret_cast<f16x4*>(Zhl + rr * 2 * KP + KP + c) = l4;
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            *reinterpret_cast<f16x8*>(Zhl + rr * 2 * KP + c0 + 8 * k) = h8[k];
+            *reinterpret_cast<f16x8*>(Zhl + rr * 2 * KP + KP + c0 + 8 * k) = l8[k];
+          }
         }
       }
-     }
     }
+  };
+  int64_t t = (int64_t)blockIdx.x * RBF_WAVES + wave;
+  f32x4 xa[NK][2], xb[NK][2];
+  if (t < ntile) xload(t, xa);
+  if (t + tstep < ntile) xload(t + tstep, xb);
+  for (; t < ntile; t += 2 * tstep) {
+    tile(t, xa, t + 2 * tstep);
+    if (t + tstep >= ntile) break;
+    tile(t + tstep, xb, t + 3 * tstep);
   }
 }
 
