@@ -173,12 +173,17 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
       for (int n = 0; n < N; ++n) rp[(w * S + j) * 8 + n] = v[n];
     }
     __syncthreads();
+    // readout split over the four lane groups: group g combines waves g·NW/4 .. of the slot's partials
+    // and the lane-group sum finishes (2 LDS reads per value and lane at NW = 8 instead of 8), in the
+    // fixed order ((w0 w1)(w2 w3))((w4 w5)(w6 w7)), bit-identical in every lane of the slot
+    constexpr int WPG = NW / 4;
 #pragma unroll
     for (int n = 0; n < N; ++n) {
-      double t = rp[j * 8 + n];
+      double t = rp[((WPG * g) * S + j) * 8 + n];
 #pragma unroll
-      for (int u = 1; u < NW; ++u) t = n < NSUM ? t + rp[(u * S + j) * 8 + n] : fmax(t, rp[(u * S + j) * 8 + n]);
-      v[n] = t;
+      for (int u = 1; u < WPG; ++u)
+        t = n < NSUM ? t + rp[((WPG * g + u) * S + j) * 8 + n] : fmax(t, rp[((WPG * g + u) * S + j) * 8 + n]);
+      v[n] = n < NSUM ? rows4<false>(t) : rows4<true>(t);
     }
   };
 

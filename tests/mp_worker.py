@@ -27,12 +27,15 @@ def main():
     from albedo_amd.synthetic import SynthSpec, generate
     from oracle import spark_als as O
     lib = L.load()
-    d = generate(SynthSpec(1200, 400, 16000, seed=41))
+    big = mode == "gpubig"
+    # gpubig: a c4-shaped problem large enough that every rank's shard has light and heavy rows in each
+    # of its 4 solve chunks (and split-K rows at the default 8192-rating chunk); one sweep
+    d = generate(SynthSpec(60000, 12000, 2_000_000, zipf_s=0.8, seed=43) if big else SynthSpec(1200, 400, 16000, seed=41))
     B = O.make_blocks(d["user"], d["item"], d["rating"])
     rng = np.random.default_rng(3)
     U0 = rng.standard_normal((len(B.user_ids), k)).astype(np.float32)
     V0 = rng.standard_normal((len(B.item_ids), k)).astype(np.float32)
-    if mode in ("gpu", "gpunn"):
+    if mode in ("gpu", "gpunn", "gpubig"):
         def allreduce(_u, buf, n):
             t = torch.from_numpy(np.ctypeslib.as_array(buf, shape=(n,)))
             dist.all_reduce(t)
@@ -49,7 +52,7 @@ def main():
         ar, ag = L.ALLREDUCE_FN(allreduce), L.ALLGATHER_FN(allgather)
         p = L.als_params()
         L.check(lib.als_params_default(C.byref(p)))
-        p.rank, p.implicit_prefs, p.reg_param, p.alpha, p.max_iter = k, 1, 0.5, 40.0, 3
+        p.rank, p.implicit_prefs, p.reg_param, p.alpha, p.max_iter = k, 1, 0.5, 40.0, 1 if big else 3
         p.nonnegative = 1 if mode == "gpunn" else 0
         h = C.c_void_p()
         L.check(lib.als_create(C.byref(p), C.byref(h)))
@@ -66,6 +69,13 @@ def main():
             f = np.empty((n, k), np.float32)
             L.check(lib.als_get_factors(h, side, None, L.ptr(f, C.c_float)))
             res[name] = f
+        if big:
+            if rank == 0:
+                np.savez(out, **res)
+            lib.als_destroy(h)
+            dist.barrier()
+            dist.destroy_process_group()
+            return
         # recommendForAllUsers(10), users sharded across the ranks, lists all-gathered
         n_u = lib.als_num_rows(h, 0)
         ids = np.empty((n_u, 10), np.int32)

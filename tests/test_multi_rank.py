@@ -108,3 +108,41 @@ def test_sharded_fit_gpu_matches_single(gpu_lib, tmp_path, world, nonneg, split,
     assert np.array_equal(res["topk_sc"].view(np.uint32), ref_sc.view(np.uint32))
     for r in range(1, world):
         assert np.array_equal(np.load(out + f".rank{r}.npy"), ref_ids)
+
+
+@pytest.mark.gpu
+def test_sharded_sweep_gpu_c4_shaped(gpu_lib, tmp_path):
+    """A c4-shaped problem (60K users x 12K repos, 2M stars, rank 128) on 2 ranks sharing the GPU: each
+    rank's shard crosses all 4 solve chunks with light (light16 on the user side, D = 32 / 64) and
+    wave-kernel rows in every chunk, and split-K repos (> 8192 stars) at the default chunk, so the chunked solve and its gathers
+    run with a realistic degree mix.  One sweep (item half from U0, user half from the engine's items)
+    against the C fp64 restatement of Spark's normal-equation solve, row by row."""
+    import ctypes as C
+    from albedo_amd import _lib as L
+    from albedo_amd.synthetic import SynthSpec, generate
+    from oracle import cbind
+    k, world = 128, 2
+    d = generate(SynthSpec(60000, 12000, 2_000_000, zipf_s=0.8, seed=43))
+    B = O.make_blocks(d["user"], d["item"], d["rating"])
+    # the engine's own shard plan: every (rank, chunk) of both sides holds light and heavy rows
+    for ptr in (B.i_ptr, B.u_ptr):
+        n = len(ptr) - 1
+        starts = np.empty(world + 1, np.int64)
+        L.check(gpu_lib.als_host_plan_shards(L.ptr(np.ascontiguousarray(ptr), C.c_int64), n, world,
+                                             L.ptr(starts, C.c_int64)))
+        deg = np.diff(ptr)
+        chpad = -(-int(np.max(np.diff(starts))) // 4)
+        for r in range(world):
+            for q in range(4):
+                lo = starts[r] + q * chpad
+                dq = deg[lo:min(starts[r + 1], lo + chpad)]
+                assert np.any(dq <= 64) and np.any(dq > 64), (r, q)
+    assert np.max(np.diff(B.i_ptr)) > 8192  # split-K rows
+    rng = np.random.default_rng(3)
+    U0 = rng.standard_normal((len(B.user_ids), k)).astype(np.float32)
+    res = _launch("gpubig", str(tmp_path / "big.npz"), world=world, k=k, timeout=600)
+    V_ref = cbind.half_sweep(U0, B.i_ptr, B.i_col, B.i_val, reg=0.5, alpha=40.0)
+    U_ref = cbind.half_sweep(res["V"], B.u_ptr, B.u_col, B.u_val, reg=0.5, alpha=40.0)
+    for got, ref in ((res["V"], V_ref), (res["U"], U_ref)):
+        err = np.linalg.norm(got - ref, axis=1) / np.maximum(np.linalg.norm(ref, axis=1), 1e-30)
+        assert np.max(err) < 1e-4, np.max(err)
