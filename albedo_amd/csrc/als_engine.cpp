@@ -349,8 +349,13 @@ int split_chunk_len() {
 // rows of higher degree take solve_nnls_kernel.
 constexpr int BATCH_SLOTS[5] = {16, 8, 4, 2, 1};
 constexpr int BATCH_MIN_SLOTS = 8;
+int nnls_min_slots() {  // ALBEDO_NNLS_MIN_SLOTS: A/B knob (16, 8, 4, 2 or 1)
+  const char* e = std::getenv("ALBEDO_NNLS_MIN_SLOTS");
+  const int v = e && *e ? std::atoi(e) : BATCH_MIN_SLOTS;
+  return (v == 16 || v == 8 || v == 4 || v == 2 || v == 1) ? v : BATCH_MIN_SLOTS;
+}
 int64_t nnls_batch_rows_limit(const als_ctx* c, int v) {
-  if (BATCH_SLOTS[v] < BATCH_MIN_SLOTS) return 0;
+  if (BATCH_SLOTS[v] < nnls_min_slots()) return 0;
   return std::min<int64_t>(nnls_batch_max_degree(c->KP, BATCH_SLOTS[v]), light_limit(c));
 }
 

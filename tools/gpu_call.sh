@@ -21,11 +21,16 @@ for s in "$@"; do
     bench_c4) timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_c4.json 2> gpurun_out/bench_c4.err ;;
     bench_c2) timeout -k 10 300 python -u bench.py --config c2 --steps 10 --warmup 5 > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.err ;;
     bench_c5cpu) timeout -k 10 600 python -u bench.py --config c5 --steps 2 --warmup 1 --topk-users 0 > gpurun_out/bench_c5cpu.json 2> gpurun_out/bench_c5cpu.err ;;
+    bench_c5_s*) ALBEDO_NNLS_MIN_SLOTS=${s#bench_c5_s} timeout -k 10 400 python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
+    tests_mrbig) timeout -k 10 900 $PYT tests/test_multi_rank.py -k c4_shaped > gpurun_out/tests_mrbig.log 2>&1 ;;
+    batchtime4) (cd tools/probe && timeout -k 5 120 ./batchtime 256 16 500000 200000 6 && timeout -k 5 120 ./batchtime 256 8 500000 100000 12 && timeout -k 5 120 ./batchtime 256 4 500000 50000 24) > gpurun_out/batchtime4.txt 2>&1 ;;
     bench_c5) timeout -k 10 400 python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err ;;
     prof_c4) timeout -k 10 1100 tools/prof.sh c4 r03 16384 > gpurun_out/prof_c4.log 2>&1 ;;
     prof_c4r4) timeout -k 10 1100 tools/prof.sh c4 r04 16384 > gpurun_out/prof_c4r4.log 2>&1 ;;
     prof_c5r4) timeout -k 10 900 tools/prof.sh c5 r04 0 > gpurun_out/prof_c5r4.log 2>&1 ;;
     prof_c4r5) timeout -k 10 1100 tools/prof.sh c4 r05 0 > gpurun_out/prof_c4r5.log 2>&1 ;;
+    prof_c4r6) timeout -k 10 1100 tools/prof.sh c4 r06 0 > gpurun_out/prof_c4r6.log 2>&1 ;;
+    prof_c5r6) timeout -k 10 900 tools/prof.sh c5 r06 0 > gpurun_out/prof_c5r6.log 2>&1 ;;
     prof_c5r5) timeout -k 10 900 tools/prof.sh c5 r05 0 > gpurun_out/prof_c5r5.log 2>&1 ;;
     pmc_topk5) timeout -k 10 700 tools/pmc_topk5.sh r05 > gpurun_out/pmc_topk5.log 2>&1 ;;
     multi) # back-to-back processes on one box (each a fresh context on memory the previous one freed)
