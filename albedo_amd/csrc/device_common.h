@@ -11,6 +11,12 @@
 namespace albedo {
 
 #define WAVE_LDS_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+// Compiler-only barrier for lanes of ONE wave exchanging data through LDS: a wave's LDS operations
+// execute in order, so no wait is needed, but without it the compiler may forward a lane's own
+// (possibly conditional) store to a later load of the same address that another lane wrote, or
+// move the load above the store (r06: a y store under `if (i16 == 0)` folded into the back
+// substitution's load of it)
+#define WAVE_LDS_FENCE() asm volatile("" ::: "memory")
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 

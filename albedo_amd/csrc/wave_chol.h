@@ -164,23 +164,22 @@ __device__ __forceinline__ float sum16_all(float x) {
 // lo, so the operands come straight from the C/D registers) instead of four f32 MFMAs: 32 instead of
 // 128 matrix-core cycles per tile update.  The caller scales the system so that every U entry is
 // below 2^14 (|U_ij| <= sqrt(A_jj): max diagonal < 2^28), keeping hi and lo in fp16's normal range.
-// Scratch (floats): the diagonal tile's row image at 0, then one L⁻¹ image per panel (row-major), then
-// y (16 per panel).  Images have a row stride of 20 floats (80 B): the 16 rows a ds_read_b128 lane
-// group reads start on 16 disjoint 4-bank groups, and the four rows 4g + r the C/D reads of lane
-// group g touch sit 16 banks apart.
+// Scratch (floats): one L⁻¹ image per panel (row-major), then y (16 per panel).  Images have a row
+// stride of 20 floats (80 B): the four rows 4g + r the C/D reads of lane group g touch sit 16 banks
+// apart.
 constexpr int WCHOL_RS = 20, WCHOL_IMG = 16 * WCHOL_RS;
-__host__ __device__ constexpr int wchol_scratch_floats(int nq) { return WCHOL_IMG * (nq + 1) + 16 * nq; }
+__host__ __device__ constexpr int wchol_scratch_floats(int nq) { return WCHOL_IMG * nq + 16 * nq; }
 
 template <int NQ, bool SPLIT = false>
 __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2], float (&bacc)[NQ], float* scr,
                                                 float (&xs)[NQ]) {
   const int lane = threadIdx.x & 63, q = lane >> 4, i16 = lane & 15;
-  float* s_y = scr + WCHOL_IMG * (NQ + 1);  // y of every panel in the lane-group layout
+  float* s_y = scr + WCHOL_IMG * NQ;  // y of every panel in the lane-group layout
   bool notpd = false;
   WCHOL_T0();
   static_for<0, NQ>([&](auto JB) {
     constexpr int jb = decltype(JB)::value, td = tix(jb, jb, NQ);
-    float* img = scr + WCHOL_IMG * (jb + 1);  // this panel's L⁻¹, row-major
+    float* img = scr + WCHOL_IMG * jb;  // this panel's L⁻¹, row-major
     WCHOL_PH(0);
     bool np;
     const f32x4 lv = elim16_inverse(acc[td], i16, q, np);  // lane i + 16q: L⁻¹[i][4q .. 4q+3]
@@ -197,6 +196,7 @@ __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2],
       acc[t] = u;
     });
     // lane c + 16g: L⁻¹[4g + r][c] (the LDS pipe is in order: the image stores above come first)
+    WAVE_LDS_FENCE();
     float lc[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) lc[r] = img[WCHOL_RS * (4 * q + r) + i16];
@@ -247,8 +247,7 @@ __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2],
       bacc[M] -= rows4_sum(pv);
     });
     WCHOL_PH(4);
-    WAVE_LDS_SYNC();  // scratch reads done before the next panel rewrites the row image
-    WCHOL_PH(5);
+    WAVE_LDS_FENCE();  // the y store before any later read of it
   });
 
   // ---- back substitution: x_jb = L_jb⁻ᵀ (y_jb - Σ_{M > jb} U(jb, M) x_M), right-looking: as soon as
@@ -261,7 +260,7 @@ __device__ __forceinline__ bool wave_chol_solve(f32x4 (&acc)[NQ * (NQ + 1) / 2],
     for (int r = 0; r < 4; ++r) pr[b][r] = 0.f;
   static_for<0, NQ>([&](auto KK) {
     constexpr int jb = NQ - 1 - decltype(KK)::value;
-    const float* img = scr + WCHOL_IMG * (jb + 1);
+    const float* img = scr + WCHOL_IMG * jb;
     const f32x4 yb = ld4(s_y + 16 * jb + 4 * q);  // y[4g .. 4g+3]
     float xp = 0.f;
 #pragma unroll

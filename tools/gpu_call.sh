@@ -11,6 +11,7 @@ for s in "$@"; do
   case $s in
     bounds_c2) timeout -k 10 300 python -u tools/topk_bounds.py --config c2 --sweeps 10 --sample 16384 --out gpurun_out/bounds_c2_s10.json > gpurun_out/bounds_c2.log 2>&1 ;;
     bounds_c4) timeout -k 10 500 python -u tools/topk_bounds.py --config c4 --sweeps 25 --sample 16384 --out gpurun_out/bounds_c4_s25.json > gpurun_out/bounds_c4.log 2>&1 ;;
+    tq_*) n=${s#tq_}; ALBEDO_ALS_LIB=$PWD/tools/ab/$n.so timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "half_sweep or golden or facade or albedo_protocol" > gpurun_out/$s.log 2>&1 ;;
     tests_quick) timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "half_sweep or golden or facade or albedo_protocol" > gpurun_out/tests_quick.log 2>&1 ;;
     tests_topk) timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_recommenders.py -k "topk or ndcg or recommend or transform or facade or albedo" > gpurun_out/tests_topk.log 2>&1 ;;
     tests_scale) timeout -k 10 900 $PYT tests/test_gpu_scale.py -s > gpurun_out/tests_scale.log 2>&1 ;;
