@@ -208,7 +208,7 @@ def main():
     # counter passes of this config (tools/prof.sh -> tools/sqsum.py; PMC cannot run inside the bench)
     mfma_evidence = None
     def latest(stem):  # the newest round's committed profile of this config
-        for tag in ("r05", "r04"):
+        for tag in ("r06", "r05", "r04"):
             path = os.path.join(ROOT, "profiles", f"{tag}_{args.config}_{stem}.json")
             if os.path.exists(path):
                 return path
