@@ -71,16 +71,10 @@ __device__ __forceinline__ bool entry_valid(const SolveArgs& a, float r, int i16
 // the Cholesky steps and the x' stage: K is block diagonal (the cross block is zeroed), so the
 // factorisation of one block never touches the other (L's cross entries stay exactly 0), and each
 // row's arithmetic is the one it would get alone.
-// DM > 0 (ALBEDO_L16_DM builds, r04's reverted degree-specialised units): DM bounds the degrees of
-// the unit's rows at compile time and the Cholesky and both substitutions walk the columns c < DM of
-// each block (PAIR: (c & 7) < DM) with no per-column tests; a column at or past its own row's degree
-// is an identity row (K[c][c] = 1, zero off the diagonal: its entry gathered the zero row) with
-// right-hand side 0, so its step leaves every value unchanged.  DM = 0: the live columns are tested at
-// run time (the shipped kernel).
-template <bool PAIR, int DM>
-__device__ __forceinline__ constexpr bool l16_live_ct(int c) { return DM == 0 || (PAIR ? (c & 7) < DM : c < DM); }
-
-template <int KP, bool PAIR, int DM>
+// The live columns of a unit are tested at run time (wave-uniform degrees in SGPRs).  r04's
+// degree-specialised units and the NaN-fill debug build (r05's light16 determinism probes) are not
+// part of this kernel: tools/probe/history_builds.sh rebuilds them from the commits that had them.
+template <int KP, bool PAIR>
 __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB, float r, int colE,
                                              const f32x4 (&zf)[KP / 16], float* st, float* sdlA, float* sdlB,
                                              float* vsh, const float* s_lam, const float* s_csi,
@@ -88,13 +82,6 @@ __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB,
   constexpr int NQ = KP / 32, NHC = KP / 64;
   const int lane = threadIdx.x & 63, g = lane >> 4, i16 = lane & 15;
   const int blk = PAIR ? (i16 >> 3) : 0, el = PAIR ? (i16 & 7) : i16;  // this lane's row and entry
-#ifdef ALBEDO_DEBUG_NANFILL
-  // debug builds: the wave's scratch (K / L transposition + x' stage, D^-1/2 of both rows, v) is NaN at
-  // unit entry, so any read of a value this unit did not write shows up as NaN in the factors
-  WAVE_LDS_SYNC();
-  for (int e = lane; e < 16 * L16_SLD + 2 * KP + 16; e += 64) st[e] = __builtin_nanf("");
-  WAVE_LDS_SYNC();
-#endif
   const int dme = (PAIR && blk) ? dB : dA;
   float ce = 0.f, we = 0.f;
   if (el < dme) rating_weights(r, a.implicit, a.alpha, ce, we);
@@ -170,9 +157,8 @@ __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB,
 #pragma unroll
     for (int e = 0; e < 4; ++e) kr[4 * u + e] = v[e];
   }
-  // live column c: an entry of its row (c < dA, or PAIR: block B's c - 8 < dB); DM > 0: every column
-  // below the compile-time bound
-  auto live = [&](int c) { return DM > 0 ? true : (PAIR ? (c < 8 ? c < dA : c - 8 < dB) : c < dA); };
+  // live column c: an entry of its row (c < dA, or PAIR: block B's c - 8 < dB)
+  auto live = [&](int c) { return PAIR ? (c < 8 ? c < dA : c - 8 < dB) : c < dA; };
 
   // Cholesky K = L Lᵀ over the live columns (lane i holds row i: kr[m] = L[i][m], m <= i), with the
   // forward substitution L y = C⁻¹ w in the same steps; broadcasts of lane c by DPP row_newbcast
@@ -181,7 +167,6 @@ __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB,
   static_for<0, 16>([&](auto cc) {
     constexpr int c = decltype(cc)::value;
     constexpr int cend = (PAIR && c < 8) ? 8 : 16;  // PAIR: the other block's rows are untouched
-    if constexpr (!l16_live_ct<PAIR, DM>(c)) return;
     if (!live(c)) return;
     // compiler-scheduled DPP broadcasts (bc16), not the asm helpers of device_common.h: with the asm
     // row_newbcast FMAs this kernel gave wrong results for a few paired rows from one run to the
@@ -195,7 +180,6 @@ __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB,
     dg = (i16 == c) ? inv : dg;
     static_for<c + 1, cend>([&](auto mm) {
       constexpr int m = decltype(mm)::value;
-      if constexpr (!l16_live_ct<PAIR, DM>(m)) return;
       if (!live(m)) return;
       kr[m] = fmaf(-bc16<m>(kr[c]), kr[c], kr[m]);
     });
@@ -215,7 +199,6 @@ __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB,
   for (int m = 0; m < 16; ++m) lt[m] = st[m * L16_LDK + i16];  // L[m][i16] (m >= i16 used)
   static_for<0, 16>([&](auto cc) {
     constexpr int c = 15 - decltype(cc)::value;
-    if constexpr (!l16_live_ct<PAIR, DM>(c)) return;
     if (!live(c)) return;
     const float vc = bc16<c>(y * dg);
     y = (i16 < c) ? fmaf(-lt[c], vc, y) : ((i16 == c) ? vc : y);
@@ -226,7 +209,7 @@ __device__ __forceinline__ void light16_unit(const SolveArgs& a, int dA, int dB,
   // entries 8(l >> 5) + u.  Single row: u < min(8, d), the two halves meet by one cross-half shuffle;
   // PAIR: half 0 is row A, half 1 row B (u < max(dA, dB): absent entries are zero rows with v = 0).
   const int eh = lane >> 5, cl = 2 * (lane & 31);
-  const int nu = DM > 0 ? (PAIR ? DM : (DM < 8 ? DM : 8)) : (PAIR ? (dA > dB ? dA : dB) : (dA < 8 ? dA : 8));
+  const int nu = PAIR ? (dA > dB ? dA : dB) : (dA < 8 ? dA : 8);
   const float* sdo = (PAIR && eh) ? sdlB : sdlA;
 #pragma unroll
   for (int h = 0; h < KP / L16_COLS; ++h) {
@@ -327,39 +310,7 @@ __global__ __launch_bounds__(256, KP <= 128 ? 5 : 4) void solve_light16_kernel(S
   Unit uC = unit(uidx + 2 * nw);
   for (;;) {
     f32x2 xo[KP / L16_COLS];
-#ifdef ALBEDO_L16_DM
-    // the unit's code specialised on its degree bound (r04's reverted variant, ALBEDO_L16_DM builds)
-    auto run = [&](auto dm) {
-      light16_unit<KP, PAIR, decltype(dm)::value>(a, uA.a.w, uA.b.w, r, colE, zf, st, sdlA, sdlB, vsh, s_lam, s_csi, xo);
-    };
-    using std::integral_constant;
-    const int dmax = PAIR ? (uA.a.w > uA.b.w ? uA.a.w : uA.b.w) : uA.a.w;  // wave-uniform (scalar loads)
-    if constexpr (PAIR) {
-      switch (dmax) {
-        case 0: case 1: run(integral_constant<int, 1>{}); break;
-        case 2: run(integral_constant<int, 2>{}); break;
-        case 3: run(integral_constant<int, 3>{}); break;
-        case 4: run(integral_constant<int, 4>{}); break;
-        case 5: run(integral_constant<int, 5>{}); break;
-        case 6: run(integral_constant<int, 6>{}); break;
-        case 7: run(integral_constant<int, 7>{}); break;
-        default: run(integral_constant<int, 8>{}); break;
-      }
-    } else {
-      switch (dmax) {
-        case 0: case 1: case 2: case 3: case 4: case 5: case 6: case 7: case 8: case 9: run(integral_constant<int, 9>{}); break;
-        case 10: run(integral_constant<int, 10>{}); break;
-        case 11: run(integral_constant<int, 11>{}); break;
-        case 12: run(integral_constant<int, 12>{}); break;
-        case 13: run(integral_constant<int, 13>{}); break;
-        case 14: run(integral_constant<int, 14>{}); break;
-        case 15: run(integral_constant<int, 15>{}); break;
-        default: run(integral_constant<int, 16>{}); break;
-      }
-    }
-#else
-    light16_unit<KP, PAIR, 0>(a, uA.a.w, uA.b.w, r, colE, zf, st, sdlA, sdlB, vsh, s_lam, s_csi, xo);
-#endif
+    light16_unit<KP, PAIR>(a, uA.a.w, uA.b.w, r, colE, zf, st, sdlA, sdlB, vsh, s_lam, s_csi, xo);
     const Unit done = uA;
     uidx += nw;
     if (uidx >= nu_) {
