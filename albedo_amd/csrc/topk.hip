@@ -330,13 +330,10 @@ __global__ __launch_bounds__(256, (TkScan<KP, G>::OCC)) void topk_scan_kernel(To
     if (lane < TOPK_CF / 4)
       __builtin_amdgcn_global_load_lds((tk_glb_vp)(cf + 4 * lane), (tk_lds_vp)(base + C::CB + wave * 64), 16, 0, 0);
   };
-  int64_t c_iss = -1, n_iss = 0;
+  int64_t c_iss = -1;
   for (int u = 0; u < C::NSTG - 1; ++u) {
     c_iss = next_chunk(c_iss, win_iss);
-    if (c_iss < nch) {
-      dma(c_iss, u);
-      ++n_iss;
-    }
+    if (c_iss < nch) dma(c_iss, u);
   }
 
   // the bound test's src features (s_P, ‖s_⊥‖, margin) and thresholds of this lane's rows
@@ -473,18 +470,16 @@ __global__ __launch_bounds__(256, (TkScan<KP, G>::OCC)) void topk_scan_kernel(To
   int64_t it = 0, n_scored = 0;  // chunk iterations; chunks this wave scored (its `need` held)
   for (int64_t c = next_chunk(-1, win_use); c < nch; c = next_chunk(c, win_use), ++it) {
     TKPH(5);  // next_chunk (mask walk)
-    // this wave's DMAs of chunk c have landed (in-order VM counter; later list stores only make the
-    // wait stricter), then one barrier publishes every wave's part and retires the previous slot
-    if (n_iss - it - 1 >= C::NSTG - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NVM * (C::NSTG - 2)) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this wave's DMAs of chunk c have landed, then one barrier publishes every wave's part and retires
+    // the previous slot.  vmcnt(0): r05 waited with a hand-counted vmcnt(NVM·(NSTG−2)), which assumed the
+    // VM counter retires the LDS-DMA loads and the later list stores in issue order; the plain drain
+    // measured no slower (c4 all users, scan 186.9 vs 192.1 ms, profiles/r06_bench_c4_topk_vmcnt0.json)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (c_iss < nch) {
       c_iss = next_chunk(c_iss, win_iss);
-      if (c_iss < nch) {
-        dma(c_iss, (int)((it + C::NSTG - 1) % C::NSTG));
-        ++n_iss;
-      }
+      if (c_iss < nch) dma(c_iss, (int)((it + C::NSTG - 1) % C::NSTG));
     }
     TKPH(0);  // DMA wait + barrier + next DMA issue
     TKPH_N(0, 1);
