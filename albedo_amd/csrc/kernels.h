@@ -84,6 +84,9 @@ hipError_t launch_solve_wave(int KP, const SolveArgs& a, hipStream_t s);
 
 // nonnegative = true: Spark NNLS per row; Gt = the src Gram in the NNLS tile layout (fp32).
 hipError_t launch_solve_nnls(int KP, const SolveArgs& a, const float* Gt, hipStream_t s);
+// KP = 256 per-row NNLS on 512-thread workgroups, two per CU (nnls_row.hip); launch_solve_nnls
+// routes KP = 256 here unless ALBEDO_NNLS_ROW=1024 (the register kernel of als_kernels.hip)
+hipError_t launch_solve_nnls_row256(const SolveArgs& a, const float* Gt, hipStream_t s);
 int nnls_gtile_floats(int KP);
 // NNLS rows of low degree, `slots` (16/8/4/2/1) per workgroup in lockstep (nnls_batch.hip); a slot
 // holds rows of degree <= nnls_batch_max_degree(KP, slots).  A persistent grid of at most n_cu

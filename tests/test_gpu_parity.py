@@ -741,6 +741,52 @@ def test_nnls_rank256(gpu_lib):
     assert _rel(V, V_ref) < 1e-3
 
 
+@pytest.mark.parametrize("kernel", ["512", "1024"])
+def test_nnls_rank256_per_row_kernels(gpu_lib, monkeypatch, kernel):
+    """The rank-256 per-row NNLS kernels (nnls_row.hip: 512 threads, two rows per CU, upper tiles in
+    registers; als_kernels.hip: 1024 threads, all of A in registers; ALBEDO_NNLS_ROW picks) on rows of
+    degree 100-900, against the fp64 oracle: factors within 1e-3, every row stopped by Spark's rule
+    before the iteration cap (a wrong A·v or vᵀAv still converges through the residual refreshes but
+    runs to the cap), and the same iteration count as the other kernel to within 15 %."""
+    from albedo_amd import _lib as L
+    from albedo_amd.synthetic import SynthSpec, generate
+    d = generate(SynthSpec(1200, 40, 14000, seed=47))
+    B = O.make_blocks(d["user"], d["item"], d["rating"])
+    k = 256
+    rng = np.random.default_rng(9)
+    U0 = np.abs(rng.standard_normal((len(B.user_ids), k))).astype(np.float32)
+    U0 /= np.linalg.norm(U0, axis=1, keepdims=True)
+    U0[:, ::5] *= -1.0  # some coordinates end on the wall
+    V_ref = O.half_sweep(U0, B.i_ptr, B.i_col, B.i_val, reg=0.5, alpha=40.0, nonnegative=True)
+    its = {}
+    for kern in (kernel, "1024" if kernel == "512" else "512"):
+        monkeypatch.setenv("ALBEDO_NNLS_ROW", kern)
+        p = L.als_params()
+        L.check(gpu_lib.als_params_default(C.byref(p)))
+        p.rank, p.implicit_prefs, p.reg_param, p.alpha, p.nonnegative = k, 1, 0.5, 40.0, 1
+        c = Ctx(gpu_lib, 8)
+        h = C.c_void_p()
+        L.check(gpu_lib.als_create(C.byref(p), C.byref(h)))
+        gpu_lib.als_destroy(c.h)
+        c.h, c.rank = h, k
+        c.ratings(d["user"], d["item"], d["rating"])
+        c.inject(0, B.user_ids, U0)
+        c.inject(1, B.item_ids, np.zeros((len(B.item_ids), k), np.float32))
+        c.half(1)
+        st = np.zeros(4, np.int64)
+        L.check(gpu_lib.als_path_stats(c.h, 1, L.ptr(st, C.c_int64)))
+        assert st[2] >= 30  # the per-row kernel's rows
+        sv = np.zeros(4, np.int64)
+        L.check(gpu_lib.als_solver_stats(c.h, 1, L.ptr(sv, C.c_int64)))
+        assert sv[1] < 20 * k, f"a row ran to the iteration cap ({sv[1]})"
+        its[kern] = (sv[0] - sv[3]) / max(1, st[2])
+        _, V = c.factors(1)
+        if kern == kernel:
+            assert np.all(V >= 0)
+            assert _rel(V, V_ref) < 1e-3
+    assert abs(its["512"] - its["1024"]) <= 0.15 * its["1024"], its
+
+
 @pytest.mark.parametrize("k,wgs", [(50, 0), (50, 3), (100, 2), (256, 1)])
 def test_nnls_lockstep_light_rows(gpu_lib, monkeypatch, k, wgs):
     """Light NNLS rows run in lockstep (nnls_batch.hip), 16/8/4/2/1 rows per workgroup by degree

@@ -4,6 +4,8 @@
 // 5 r2 reduce, 6 wall min, 7 update.  G = the Gram of the random (nonnegative) src factors.
 #define ALBEDO_NNLS_TIMING
 #include "../../albedo_amd/csrc/als_kernels.hip"
+#include "../../albedo_amd/csrc/nnls_row.hip"
+#include "../../albedo_amd/csrc/heavy_wave.hip"
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -57,12 +59,38 @@ void bench(int64_t nsrc, int nrows, int deg) {
   a.Z = Z; a.ptr = ptr; a.col = col; a.val = val; a.rows = rows; a.n_rows = nrows; a.lam = lam; a.X = X;
   a.kreal = KP; a.implicit = 1; a.alpha = 40.f; a.reg = 0.5f; a.err = err; a.colscale = cs; a.iters = it;
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+  // the other per-row kernel's X first (ALBEDO_NNLS_ROW=1024 <-> the 512-thread one at KP = 256)
+  std::vector<float> xo((size_t)nrows * KP), xn((size_t)nrows * KP);
+  const char* sel = getenv("ALBEDO_NNLS_ROW");
+  const bool is_old = sel && atoi(sel) == 1024;
+  if (KP == 256) {
+    setenv("ALBEDO_NNLS_ROW", is_old ? "512" : "1024", 1);
+    launch_solve_nnls(KP, a, Gt, 0);
+    hipMemcpy(xo.data(), X, xo.size() * 4, hipMemcpyDeviceToHost);
+    setenv("ALBEDO_NNLS_ROW", is_old ? "1024" : "512", 1);
+  }
   launch_solve_nnls(KP, a, Gt, 0);
   hipMemset(it, 0, 16);
   hipEventRecord(e0, 0);
   launch_solve_nnls(KP, a, Gt, 0);
   hipEventRecord(e1, 0); hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
+  if (KP == 256) {
+    hipMemcpy(xn.data(), X, xn.size() * 4, hipMemcpyDeviceToHost);
+    double num = 0, den = 0, worst = 0; long zero_mismatch = 0;
+    for (int r = 0; r < nrows; ++r) {
+      double rn = 0, rd = 0;
+      for (int c = 0; c < KP; ++c) {
+        const double dlt = (double)xn[(size_t)r * KP + c] - xo[(size_t)r * KP + c];
+        rn = fmax(rn, fabs(dlt)); rd = fmax(rd, fabs((double)xo[(size_t)r * KP + c]));
+        zero_mismatch += (xn[(size_t)r * KP + c] == 0.f) != (xo[(size_t)r * KP + c] == 0.f);
+      }
+      num = fmax(num, rn); den = fmax(den, rd); worst = fmax(worst, rd > 0 ? rn / rd : rn);
+    }
+    int herr = 0; hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost);
+    printf("%s vs the other kernel: max|dx|/max|x| %.3e, worst row %.3e, zero-pattern mismatches %ld, err %d\n",
+           is_old ? "1024-thread" : "512-thread", den > 0 ? num / den : num, worst, zero_mismatch, herr);
+  }
   unsigned long long hit[2]; hipMemcpy(hit, it, 16, hipMemcpyDeviceToHost);
   unsigned long long ph[64][8];
   hipMemcpyFromSymbol(ph, HIP_SYMBOL(albedo_nnls_ph), sizeof(ph));
@@ -75,6 +103,19 @@ void bench(int64_t nsrc, int nrows, int deg) {
   printf("phase share (64 blocks): ");
   for (int q = 0; q < 8; ++q) printf("%d:%.3f ", q, tot[q] / s);
   printf("\ncycles per iteration (block 0..63 avg): %.0f\n", s / (hit[0] * 64.0 / nrows));
+  if (KP == 256 && !is_old) {  // the 512-thread kernel: waves 0 (owner) and 6 (diagonal groups)
+    unsigned long long nph[64][2][8];
+    hipMemcpyFromSymbol(nph, HIP_SYMBOL(albedo_nrow_ph), sizeof(nph));
+    const double its = hit[0] * 64.0 / nrows;
+    for (int w = 0; w < 2; ++w) {
+      printf("512-thread wave %d cycles per iteration by phase (0 pre-B1, 1 B1, 2 product, 3 post-product, 4 B2, 5 step, 6 refresh, 7 build/iter):", w ? 6 : 0);
+      for (int q = 0; q < 8; ++q) {
+        double t = 0; for (int b = 0; b < 64 && b < nrows; ++b) t += nph[b][w][q];
+        printf(" %.0f", t / its);
+      }
+      printf("\n");
+    }
+  }
   (void)iters;
 }
 int main(int argc, char** argv) {
