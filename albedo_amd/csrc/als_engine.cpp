@@ -1657,7 +1657,7 @@ int topk_dst_basis(als_ctx* c, const Side& T, TopkPlan& P, std::vector<double>& 
 // The lists still hold 64 and the best 64 are rescored.
 // the running threshold's rank in the candidate lists: k + 16 (c4 all users after 25 sweeps: k + 8 /
 // 12 / 16 / 24 -> 33.6 / 47.6 / 50.7 / 46.9M users/s; fewer leave more rows to the exact rescan)
-int topk_threshold_rank(int k) { return std::max(k, std::min(TOPK_KC, k + 16)); }
+int topk_threshold_rank(int k) { return std::max(k, std::min(TOPK_KC, k + ALBEDO_TOPK_KT_EXTRA)); }
 
 int topk_plan(als_ctx* c, int src, int k, TopkPlan& P) {
   P.src = src;
@@ -1709,7 +1709,7 @@ int topk_plan(als_ctx* c, int src, int k, TopkPlan& P) {
   HIPCHK(P.d_tp.ensure((size_t)nn * TOPK_M * 8));
   HIPCHK(P.d_cfeat.ensure((size_t)std::max<int64_t>(P.n_chunks, 1) * TOPK_CF * 4));
   HIPCHK(P.d_supf.ensure((size_t)std::max<int64_t>(P.n_super, 1) * TOPK_CF * 4));
-  HIPCHK(P.d_probe.ensure((size_t)256 * KP * 2));
+  HIPCHK(P.d_probe.ensure((size_t)TOPK_NPROBE * KP * 2));
   const size_t tb = topk_sort_temp_bytes(T.n);
   HIPCHK(P.d_tmp.ensure(std::max<size_t>(tb, 16)));
   if (T.n > 0)

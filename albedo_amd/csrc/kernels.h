@@ -182,6 +182,19 @@ struct TopkArgs {
   int order_dir_bits;           // order: key bits of the direction s_P / ‖s‖ (bytes: u1, u2, u3; 0: depth only)
 };
 constexpr int TOPK_KC = 64;     // candidates rescored exactly per src row (k <= 64)
+#ifndef ALBEDO_TOPK_NPROBE
+#define ALBEDO_TOPK_NPROBE 512
+#endif
+constexpr int TOPK_NPROBE = ALBEDO_TOPK_NPROBE;  // probe rows of the starting thresholds (largest norms)
+#ifndef ALBEDO_TOPK_BISECT
+#define ALBEDO_TOPK_BISECT 16
+#endif
+// bisection steps of the probe threshold: the top bits of the order-preserving key; fewer than 32 leave
+// a lower bound of the kt-th probe score (valid, coarser by the undecided bits)
+constexpr int TOPK_BISECT = ALBEDO_TOPK_BISECT;
+#ifndef ALBEDO_TOPK_KT_EXTRA
+#define ALBEDO_TOPK_KT_EXTRA 16
+#endif
 constexpr int TOPK_CAP = 128;   // candidate list capacity per src row (compacted to 64 above TOPK_TRIG)
 constexpr int TOPK_TRIG = 112;  // compaction trigger: frequent enough that thresholds follow the running kt-th best
 constexpr int TOPK_MAX = 512;   // k above TOPK_KC: exact full scan (topk_exact_kernel)

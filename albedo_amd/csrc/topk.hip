@@ -731,11 +731,12 @@ __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_
     spd[d] += __shfl_xor(spd[d], 32);
   }
   const char* Pr = reinterpret_cast<const char*>(a.probe);
-  const int64_t n_probe = a.n_dst < 256 ? a.n_dst : 256;
+  constexpr int NPJ = TOPK_NPROBE / 16;
+  const int64_t n_probe = a.n_dst < TOPK_NPROBE ? a.n_dst : TOPK_NPROBE;
   // order-preserving uint keys of the 256 scores: lane (i16, g) holds column 16J + i16 of rows 4g + r
-  uint32_t u[16][4];
+  uint32_t u[NPJ][4];
 #pragma unroll
-  for (int J = 0; J < 16; ++J) {
+  for (int J = 0; J < NPJ; ++J) {
     const int64_t p = 16 * J + i16;
     f32x4 acc = zero4();
 #pragma unroll
@@ -761,15 +762,15 @@ __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_
     c += __builtin_amdgcn_mov_dpp(c, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]: lane i^1
     return c;
   };
-  uint32_t lo[4] = {0u, 0u, 0u, 0u};  // count(>= lo) >= kt always holds (256 keys >= 0)
+  uint32_t lo[4] = {0u, 0u, 0u, 0u};  // count(>= lo) >= kt always holds (TOPK_NPROBE keys >= 0)
   uint32_t hi[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-  for (int it = 0; it < 32; ++it) {
+  for (int it = 0; it < TOPK_BISECT; ++it) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const uint32_t mid = lo[r] + (uint32_t)(((uint64_t)hi[r] - lo[r] + 1) >> 1);
       int cnt = 0;
 #pragma unroll
-      for (int J = 0; J < 16; ++J) cnt += u[J][r] >= mid ? 1 : 0;
+      for (int J = 0; J < NPJ; ++J) cnt += u[J][r] >= mid ? 1 : 0;
       cnt = row_count(cnt);
       if (cnt >= a.kt) lo[r] = mid;
       else hi[r] = mid - 1u;
@@ -777,7 +778,10 @@ __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_
   }
   float vs[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) vs[r] = __uint_as_float((lo[r] & 0x80000000u) ? (lo[r] & 0x7fffffffu) : ~lo[r]);
+  // key -> the smallest score of its bucket (the undecided low bits: zero); keys at or below -inf's
+  // (0x007fffff; truncated, they would decode to NaN) are -inf
+  for (int r = 0; r < 4; ++r)
+    vs[r] = lo[r] < 0x00800000u ? -INFINITY : __uint_as_float((lo[r] & 0x80000000u) ? (lo[r] & 0x7fffffffu) : ~lo[r]);
   const int rsel = 4 * g + (i16 & 3);  // the row this lane reports in the group (lanes i16 < 4)
   const double nrm2 = __shfl(ss, rsel);
   const double nrm = sqrt(nrm2);
@@ -1243,7 +1247,7 @@ hipError_t topk_prepare(int KP, int kreal, const float* T, int64_t n, float tsc,
   e = rocprim::radix_sort_pairs_desc(temp, tb, nk0, nk1, nperm + n, nperm, (size_t)n, 0, 32, s);
   if (e != hipSuccess) return e;
   topk_pack_kernel<<<tk_grid(n_pad * KP, 256), 256, 0, s>>>(T, n, n_pad, KP, tsc, perm, reinterpret_cast<_Float16*>(Th));
-  topk_pack_kernel<<<tk_grid(256 * KP, 256), 256, 0, s>>>(T, std::min<int64_t>(n, 256), 256, KP, tsc, nperm,
+  topk_pack_kernel<<<tk_grid(TOPK_NPROBE * KP, 256), 256, 0, s>>>(T, std::min<int64_t>(n, TOPK_NPROBE), TOPK_NPROBE, KP, tsc, nperm,
                                                           reinterpret_cast<_Float16*>(probe));
   topk_chunk_feat_kernel<<<tk_grid(n_chunks, 4), 256, 0, s>>>(tp, perm, pk1, n, CH, n_chunks, cfeat);
   topk_super_feat_kernel<<<tk_grid(n_super, 256), 256, 0, s>>>(cfeat, n_chunks, n_super, supf);

@@ -45,10 +45,12 @@ for s in "$@"; do
     prof_c2) timeout -k 10 600 tools/prof.sh c2 r03 16384 > gpurun_out/prof_c2.log 2>&1 ;;
     trace_c4) mkdir -p gpurun_out/trace_c4 && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_c4 -o run -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu --topk-users 16384 > gpurun_out/trace_c4/bench.json 2> gpurun_out/trace_c4/bench.err ;;
     trace_topk) mkdir -p gpurun_out/trace_topk && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_topk -o run -- python3 -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/trace_topk/bench.json 2> gpurun_out/trace_topk/bench.err ;;
+    trace_topk4) mkdir -p gpurun_out/trace_topk4 && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_topk4 -o run -- python3 -u bench.py --no-cpu > gpurun_out/trace_topk4/bench.json 2> gpurun_out/trace_topk4/bench.err ;;
     tests_solve) timeout -k 10 700 $PYT tests/test_gpu_parity.py tests/test_gpu_heavy_tail.py tests/test_gpu_scale.py -k "half_sweep or golden or facade or albedo_protocol or column_scaling or positive_definite or heavy or c4_scale_rows or c2_scale" > gpurun_out/tests_solve.log 2>&1 ;;
     tests_nnls) timeout -k 10 700 $PYT tests/test_gpu_parity.py tests/test_gpu_heavy_tail.py tests/test_gpu_c5_rows.py -k "nnls or c5 or million" > gpurun_out/tests_nnls.log 2>&1 ;;
     nnlsrow) (for dg in "2048 200" "512 2000" "4096 60"; do set -- $dg; echo "## 512-thread rows $1 deg $2"; timeout -k 5 60 tools/probe/nnlstime 256 100000 $1 $2 || exit 1; echo "## 1024-thread rows $1 deg $2"; ALBEDO_NNLS_ROW=1024 timeout -k 5 60 tools/probe/nnlstime 256 100000 $1 $2 || exit 1; done) > gpurun_out/nnlsrow.txt 2>&1 ;;
     nnlsph) (for b in ${NNLS_PROBES:-nnlstime}; do for dg in "2048 200" "4096 60" "512 2000"; do set -- $dg; echo "## $b rows $1 deg $2"; timeout -k 5 60 tools/probe/$b 256 100000 $1 $2 || exit 1; done; done) > gpurun_out/nnlsph.txt 2>&1 ;;
+    bench_ab_*) n=${s#bench_ab_}; ALBEDO_ALS_LIB=$PWD/tools/ab/$n.so timeout -k 10 900 python -u bench.py > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
     bench_c5_old) ALBEDO_NNLS_ROW=1024 timeout -k 10 400 python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/bench_c5_old.json 2> gpurun_out/bench_c5_old.err ;;
     batchtime) (cd tools/probe && timeout -k 5 120 ./batchtime 256 16 500000 200000 6 && timeout -k 5 120 ./batchtime 256 8 500000 100000 12) > gpurun_out/batchtime.txt 2>&1 ;;
     nnlsab) (timeout -k 5 60 tools/probe/nnlstime_base 256 100000 2048 200 && timeout -k 5 60 tools/probe/nnlstime 256 100000 2048 200 && timeout -k 5 60 tools/probe/nnlstime_base 256 100000 2048 200 && timeout -k 5 60 tools/probe/nnlstime 256 100000 2048 200) > gpurun_out/nnlsab.txt 2>&1 ;;
