@@ -2019,11 +2019,23 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   // each pass is copied back before the next starts
   int pin_state = 0;  // bit 0: ids registered, bit 1: scores registered
   const size_t pin_bytes = (size_t)(hi - lo) * k * 4;
+  // Zero-copy results (r06, default): the select / exact kernels write the lists straight into the
+  // mapped caller arrays over PCIe.  The DMA pipeline (device buffers, copies of each finished range
+  // on a copy stream) moved the 4.8 GB of an all-users c4 call at ~29 GB/s and finished ~110 ms after
+  // the last kernel; written in place, the select runs at the link's rate with nothing behind it
+  // (c4 all users 0.339 -> 0.300 s).  ALBEDO_TOPK_ZEROCOPY=0: the DMA pipeline; =2: zero-copy with the
+  // select in output-slot ranges (no faster).
+  const int zmode = [] {
+    const char* e = std::getenv("ALBEDO_TOPK_ZEROCOPY");
+    return e ? std::atoi(e) : 1;
+  }();
+  bool zcopy = zmode == 1 || zmode == 2;
   auto pin = [&, dev = c->dev]() {
     if (hipSetDevice(dev) != hipSuccess) return;
-    if (hipHostRegister(dst_ids_out + lo * k, pin_bytes, hipHostRegisterDefault) != hipSuccess) return;
+    const unsigned fl = zcopy ? hipHostRegisterMapped : hipHostRegisterDefault;
+    if (hipHostRegister(dst_ids_out + lo * k, pin_bytes, fl) != hipSuccess) return;
     pin_state |= 1;
-    if (hipHostRegister(scores_out + lo * k, pin_bytes, hipHostRegisterDefault) == hipSuccess) pin_state |= 2;
+    if (hipHostRegister(scores_out + lo * k, pin_bytes, fl) == hipSuccess) pin_state |= 2;
   };
   std::thread pin_thr;
   const bool want_pin = dense_out && hi - lo > range;
@@ -2048,6 +2060,20 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
     return plan_rc;
   }
   stamp("plan (materialize dst, Gram + host eig, dst sort + fp16 pack) + pin the output arrays");
+  int32_t* zids = nullptr;
+  float* zsc = nullptr;
+  if (async_out && zcopy) {
+    void* pi = nullptr;
+    void* ps = nullptr;
+    if (hipHostGetDevicePointer(&pi, dst_ids_out + lo * k, 0) == hipSuccess &&
+        hipHostGetDevicePointer(&ps, scores_out + lo * k, 0) == hipSuccess) {
+      zids = static_cast<int32_t*>(pi);
+      zsc = static_cast<float*>(ps);
+    } else {
+      zcopy = false;
+      (void)hipGetLastError();
+    }
+  }
   hipStream_t cs = nullptr;
   hipEvent_t ev_copy[2] = {nullptr, nullptr};
   std::vector<hipEvent_t> ev_rng;  // one per finished range: the copy stream waits for it
@@ -2089,6 +2115,17 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   }
   for (int64_t it = 0; it < n_pass; ++it) {
     const int64_t q0 = pstart[it], nc = (it + 1 < n_pass ? pstart[it + 1] : hi) - q0;
+    if (async_out && zcopy) {  // results written in place by the kernels
+      // mode 2: select in output-slot order by ranges (consecutive waves write consecutive lists)
+      const int rc = topk_run_rows(c, P, rowsf(q0), q0, q0, nc, zids + (q0 - lo) * k, zsc + (q0 - lo) * k,
+                                   zmode == 2 ? range : INT64_MAX);
+      if (rc != ALS_OK) {
+        end_async();
+        return rc;
+      }
+      stamp("pass");
+      continue;
+    }
     if (async_out) {
       const int b = (int)(it & 1);
       int rc = ALS_OK;

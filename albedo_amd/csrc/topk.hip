@@ -693,7 +693,7 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
 // arithmetic and F2J's own rounding), ‖s‖ rounded up.  Sort key: thr0 / ‖s‖ (rows that stop at
 // similar depths share a workgroup), its low a.order_dir_bits bits replaced by the direction of s_P.
 template <int KP>
-__global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_t* __restrict__ key,
+__global__ __launch_bounds__(256, 2) void topk_order_key_kernel(TopkArgs a, uint32_t* __restrict__ key,
                                                              uint32_t* __restrict__ val, float* __restrict__ thr0,
                                                              float* __restrict__ sfo) {
   constexpr int NQ = KP / 32, RB = 2 * KP;
@@ -733,28 +733,11 @@ __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_
   const char* Pr = reinterpret_cast<const char*>(a.probe);
   constexpr int NPJ = TOPK_NPROBE / 16;
   const int64_t n_probe = a.n_dst < TOPK_NPROBE ? a.n_dst : TOPK_NPROBE;
-  // order-preserving uint keys of the 256 scores: lane (i16, g) holds column 16J + i16 of rows 4g + r
-  uint32_t u[NPJ][4];
-#pragma unroll
-  for (int J = 0; J < NPJ; ++J) {
-    const int64_t p = 16 * J + i16;
-    f32x4 acc = zero4();
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const f16x8 d = *reinterpret_cast<const f16x8*>(Pr + p * RB + 16 * (4 * q + g));  // zero rows past n
-      acc = mfma_h(sf[q], d, acc);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t bb = __float_as_uint(p < n_probe ? acc[r] : -INFINITY);
-      u[J][r] = (bb & 0x80000000u) ? ~bb : (bb | 0x80000000u);
-    }
-  }
-  // exact kt-th largest per row: bisection on the key (count of keys >= mid over the row's 16 lanes).
-  // The four rows' searches interleave, and each 16-lane count is a DPP butterfly (row_mirror,
-  // row_half_mirror, quad reversal, quad swap: every lane ends with the row's total) -- a __shfl_xor
-  // step is an LDS permute, and 4 x 32 x 4 of them in dependent chains made this kernel ~19 ms at
-  // 20M rows.  Integer counts: the same keys as before.
+  // exact kt-th largest per row: bisection on order-preserving uint keys (count of keys >= mid over
+  // the row's 16 lanes).  Lane (i16, g) holds probe column 16J + i16 of rows 4g + r.  Each 16-lane
+  // count is a DPP butterfly (row_mirror, row_half_mirror, quad reversal, quad swap: every lane ends
+  // with the row's total) -- a __shfl_xor step is an LDS permute, and 4 x 32 x 4 of them in dependent
+  // chains made this kernel ~19 ms at 20M rows.
   auto row_count = [](int c) {
     c += __builtin_amdgcn_mov_dpp(c, 0x140, 0xF, 0xF, false);  // row_mirror: lane i^15
     c += __builtin_amdgcn_mov_dpp(c, 0x141, 0xF, 0xF, false);  // row_half_mirror: lane i^7
@@ -762,20 +745,45 @@ __global__ __launch_bounds__(256) void topk_order_key_kernel(TopkArgs a, uint32_
     c += __builtin_amdgcn_mov_dpp(c, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]: lane i^1
     return c;
   };
+  // rows per pass: all four while their keys fit 128 VGPRs, else passes of two rows that recompute the
+  // probe scores on MFMA (1024 probes in one pass hold 256 key VGPRs: one wave per SIMD, r06 +76 ms)
+  constexpr int RP = NPJ * 4 <= 128 ? 4 : 2;
   uint32_t lo[4] = {0u, 0u, 0u, 0u};  // count(>= lo) >= kt always holds (TOPK_NPROBE keys >= 0)
-  uint32_t hi[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-  for (int it = 0; it < TOPK_BISECT; ++it) {
+  static_for<0, 4 / RP>([&](auto pc) {
+    constexpr int P0 = decltype(pc)::value * RP;
+    uint32_t u[NPJ][RP];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t mid = lo[r] + (uint32_t)(((uint64_t)hi[r] - lo[r] + 1) >> 1);
-      int cnt = 0;
+    for (int J = 0; J < NPJ; ++J) {
+      const int64_t p = 16 * J + i16;
+      f32x4 acc = zero4();
 #pragma unroll
-      for (int J = 0; J < NPJ; ++J) cnt += u[J][r] >= mid ? 1 : 0;
-      cnt = row_count(cnt);
-      if (cnt >= a.kt) lo[r] = mid;
-      else hi[r] = mid - 1u;
+      for (int q = 0; q < NQ; ++q) {
+        const f16x8 d = *reinterpret_cast<const f16x8*>(Pr + p * RB + 16 * (4 * q + g));  // zero rows past n
+        acc = mfma_h(sf[q], d, acc);
+      }
+#pragma unroll
+      for (int rr = 0; rr < RP; ++rr) {
+        const uint32_t bb = __float_as_uint(p < n_probe ? acc[P0 + rr] : -INFINITY);
+        u[J][rr] = (bb & 0x80000000u) ? ~bb : (bb | 0x80000000u);
+      }
+      if constexpr (RP < 4) __builtin_amdgcn_sched_barrier(0);  // probe loads a few columns ahead only
     }
-  }
+    uint32_t hi[RP];
+#pragma unroll
+    for (int rr = 0; rr < RP; ++rr) hi[rr] = 0xffffffffu;
+    for (int it = 0; it < TOPK_BISECT; ++it) {
+#pragma unroll
+      for (int rr = 0; rr < RP; ++rr) {
+        const uint32_t mid = lo[P0 + rr] + (uint32_t)(((uint64_t)hi[rr] - lo[P0 + rr] + 1) >> 1);
+        int cnt = 0;
+#pragma unroll
+        for (int J = 0; J < NPJ; ++J) cnt += u[J][rr] >= mid ? 1 : 0;
+        cnt = row_count(cnt);
+        if (cnt >= a.kt) lo[P0 + rr] = mid;
+        else hi[rr] = mid - 1u;
+      }
+    }
+  });
   float vs[4];
 #pragma unroll
   // key -> the smallest score of its bucket (the undecided low bits: zero); keys at or below -inf's

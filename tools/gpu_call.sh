@@ -19,6 +19,10 @@ for s in "$@"; do
     tests_all) timeout -k 10 1100 $PYT tests -m gpu > gpurun_out/tests_all.log 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke.log 2>&1 ;;
     bench_default) timeout -k 10 900 python -u bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err ;;
+    bench_trace) ALBEDO_TOPK_TRACE=1 timeout -k 10 900 python -u bench.py --no-cpu > gpurun_out/bench_trace.json 2> gpurun_out/bench_trace.err ;;
+    bench_trace_zc) ALBEDO_TOPK_ZEROCOPY=1 ALBEDO_TOPK_TRACE=1 timeout -k 10 900 python -u bench.py --no-cpu > gpurun_out/bench_trace_zc.json 2> gpurun_out/bench_trace_zc.err ;;
+    tests_topk_zc) ALBEDO_TOPK_ZEROCOPY=1 timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_recommenders.py -k "topk or ndcg or recommend or transform or facade or albedo" > gpurun_out/tests_topk_zc.log 2>&1 ;;
+    bench_trace_zc2) ALBEDO_TOPK_ZEROCOPY=2 ALBEDO_TOPK_TRACE=1 timeout -k 10 900 python -u bench.py --no-cpu > gpurun_out/bench_trace_zc2.json 2> gpurun_out/bench_trace_zc2.err ;;
     bench_c4) timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_c4.json 2> gpurun_out/bench_c4.err ;;
     bench_c2) timeout -k 10 300 python -u bench.py --config c2 --steps 10 --warmup 5 > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.err ;;
     bench_c5cpu) timeout -k 10 600 python -u bench.py --config c5 --steps 2 --warmup 1 --topk-users 0 > gpurun_out/bench_c5cpu.json 2> gpurun_out/bench_c5cpu.err ;;
@@ -46,6 +50,7 @@ for s in "$@"; do
     trace_c4) mkdir -p gpurun_out/trace_c4 && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_c4 -o run -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu --topk-users 16384 > gpurun_out/trace_c4/bench.json 2> gpurun_out/trace_c4/bench.err ;;
     trace_topk) mkdir -p gpurun_out/trace_topk && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_topk -o run -- python3 -u bench.py --steps 1 --warmup 24 --no-cpu > gpurun_out/trace_topk/bench.json 2> gpurun_out/trace_topk/bench.err ;;
     trace_topk4) mkdir -p gpurun_out/trace_topk4 && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_topk4 -o run -- python3 -u bench.py --no-cpu > gpurun_out/trace_topk4/bench.json 2> gpurun_out/trace_topk4/bench.err ;;
+    trace_topkcp) mkdir -p gpurun_out/trace_topkcp && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/trace_topkcp -o run -- python3 -u bench.py --no-cpu --steps 1 --warmup 0 > gpurun_out/trace_topkcp/bench.json 2> gpurun_out/trace_topkcp/bench.err ;;
     tests_solve) timeout -k 10 700 $PYT tests/test_gpu_parity.py tests/test_gpu_heavy_tail.py tests/test_gpu_scale.py -k "half_sweep or golden or facade or albedo_protocol or column_scaling or positive_definite or heavy or c4_scale_rows or c2_scale" > gpurun_out/tests_solve.log 2>&1 ;;
     tests_nnls) timeout -k 10 700 $PYT tests/test_gpu_parity.py tests/test_gpu_heavy_tail.py tests/test_gpu_c5_rows.py -k "nnls or c5 or million" > gpurun_out/tests_nnls.log 2>&1 ;;
     nnlsrow) (for dg in "2048 200" "512 2000" "4096 60"; do set -- $dg; echo "## 512-thread rows $1 deg $2"; timeout -k 5 60 tools/probe/nnlstime 256 100000 $1 $2 || exit 1; echo "## 1024-thread rows $1 deg $2"; ALBEDO_NNLS_ROW=1024 timeout -k 5 60 tools/probe/nnlstime 256 100000 $1 $2 || exit 1; done) > gpurun_out/nnlsrow.txt 2>&1 ;;
