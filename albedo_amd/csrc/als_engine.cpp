@@ -2022,12 +2022,13 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   // Zero-copy results (r06, default): the select / exact kernels write the lists straight into the
   // mapped caller arrays over PCIe.  The DMA pipeline (device buffers, copies of each finished range
   // on a copy stream) moved the 4.8 GB of an all-users c4 call at ~29 GB/s and finished ~110 ms after
-  // the last kernel; written in place, the select runs at the link's rate with nothing behind it
-  // (c4 all users 0.339 -> 0.300 s).  ALBEDO_TOPK_ZEROCOPY=0: the DMA pipeline; =2: zero-copy with the
-  // select in output-slot ranges (no faster).
+  // the last kernel; written in place, the select runs at the link's rate with nothing behind it.
+  // Mode 2 (default) selects in output-slot ranges, so a workgroup's four lists leave as one block of
+  // 16-B stores (c4 all users: DMA 0.339 s, mode 1 (scan order) 0.298-0.318 s, mode 2 0.291 s on the
+  // box that ran mode 1 at 0.318); ALBEDO_TOPK_ZEROCOPY=0: the DMA pipeline.
   const int zmode = [] {
     const char* e = std::getenv("ALBEDO_TOPK_ZEROCOPY");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : 2;
   }();
   bool zcopy = zmode == 1 || zmode == 2;
   auto pin = [&, dev = c->dev]() {

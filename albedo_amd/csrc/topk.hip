@@ -589,23 +589,61 @@ __device__ __forceinline__ float f2j_dot_rows(const float* __restrict__ s, const
   return row >= 0 ? acc : -INFINITY;
 }
 
+template <int KP>
+__device__ __forceinline__ void topk_select_row(const TopkArgs& a, int64_t si, int64_t so, float* stage, int* lid,
+                                                float* lsc);
+
 // One wave per src row: best 64 of the list, exact F2J rescoring, sort, certify, write top-k.
 template <int KP>
 __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
-  constexpr int CAP = TOPK_CAP, NS = CAP / 64;
   __shared__ __attribute__((aligned(16))) float s_stage[4][64 * TK_SEL_LD + KP];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int64_t si, so;  // scan position, output slot
-  if (a.in_pos) {  // a range of output slots
+  // a range of output slots (in_pos): the workgroup's four consecutive lists leave as one contiguous
+  // block of 16-B stores per array (written through PCIe into the caller's arrays, r06: whole 16-B
+  // units instead of each wave's 4-B stores over its own 4k bytes)
+  __shared__ __attribute__((aligned(16))) int s_oid[4 * TOPK_KC];
+  __shared__ __attribute__((aligned(16))) float s_osc[4 * TOPK_KC];
+  const int wave = threadIdx.x >> 6;
+  const bool grouped = a.in_pos != nullptr;
+  int64_t si = 0, so = 0;  // scan position, output slot
+  if (grouped) {
     const int64_t l = (int64_t)blockIdx.x * 4 + wave;
-    if (l >= a.n_slots) return;
-    so = a.slot0 + l;
-    si = a.in_pos[so];
-  } else {
-    si = (int64_t)blockIdx.x * 4 + wave;
-    if (si >= a.n_src) return;
-    so = a.out_pos ? (int64_t)a.out_pos[si] : si;
+    if (l < a.n_slots) {
+      so = a.slot0 + l;
+      si = a.in_pos[so];
+      topk_select_row<KP>(a, si, so, s_stage[wave], s_oid + wave * a.k, s_osc + wave * a.k);
+    }
+    __syncthreads();
+    const int64_t nu = min((int64_t)4, a.n_slots - (int64_t)blockIdx.x * 4);
+    const int64_t so0 = a.slot0 + (int64_t)blockIdx.x * 4;  // a multiple of 4: so0·k·4 B is 16-B aligned
+    const int tot = (int)nu * a.k;
+    int* oi = a.out_ids + so0 * a.k;
+    float* os = a.out_scores + so0 * a.k;
+    for (int t = threadIdx.x; 4 * t < tot; t += 256) {
+      if (4 * t + 4 <= tot) {
+        *reinterpret_cast<int4*>(oi + 4 * t) = *reinterpret_cast<const int4*>(s_oid + 4 * t);
+        *reinterpret_cast<float4*>(os + 4 * t) = *reinterpret_cast<const float4*>(s_osc + 4 * t);
+      } else {
+        for (int e = 4 * t; e < tot; ++e) {
+          oi[e] = s_oid[e];
+          os[e] = s_osc[e];
+        }
+      }
+    }
+    return;
   }
+  si = (int64_t)blockIdx.x * 4 + wave;
+  if (si >= a.n_src) return;
+  so = a.out_pos ? (int64_t)a.out_pos[si] : si;
+  topk_select_row<KP>(a, si, so, s_stage[wave], nullptr, nullptr);
+}
+
+// One src row of topk_select_kernel (a wave): best 64 of the list, exact F2J rescoring, sort, certify,
+// top-k into the output slot (or into the workgroup's LDS lists when lid / lsc are given).
+template <int KP>
+__device__ __forceinline__ void topk_select_row(const TopkArgs& a, int64_t si, int64_t so, float* stage, int* lid,
+                                                float* lsc) {
+  constexpr int CAP = TOPK_CAP, NS = CAP / 64;
+  const int lane = threadIdx.x & 63;
   const int srow = a.src_rows[si];
   const float* s = a.S + (int64_t)srow * KP;
   const int cnt = min(a.lcnt[si], CAP);
@@ -636,7 +674,7 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
   // lower bound of the true k-th).  (Each rescored candidate reads a 512-B fp32 row from HBM.)
   const bool rescore = a.n_dst <= TOPK_KC || lane < a.kt;
   const int row = (i2[0] >= 0 && rescore) ? a.perm[i2[0]] : -1;
-  const float ex = f2j_dot_rows<KP>(s, a.T, row, a.kreal, s_stage[wave]);
+  const float ex = f2j_dot_rows<KP>(s, a.T, row, a.kreal, stage);
   // ‖s‖ for the certification bound: the order kernel's value rounded up (a larger ‖s‖ only widens
   // the bound), else computed here
   double nsr = 0.0;
@@ -676,8 +714,15 @@ __global__ __launch_bounds__(256) void topk_select_kernel(TopkArgs a) {
   }
   if (lane < k) {
     const int idx = ix1[0];
-    a.out_ids[so * k + lane] = idx >= 0 ? a.dst_ids[idx] : -1;
-    a.out_scores[so * k + lane] = idx >= 0 ? sc1[0] : __int_as_float(0x7fc00000);
+    const int oid = idx >= 0 ? a.dst_ids[idx] : -1;
+    const float osc = idx >= 0 ? sc1[0] : __int_as_float(0x7fc00000);
+    if (lid) {
+      lid[lane] = oid;
+      lsc[lane] = osc;
+    } else {
+      a.out_ids[so * k + lane] = oid;
+      a.out_scores[so * k + lane] = osc;
+    }
   }
 }
 
