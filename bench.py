@@ -173,7 +173,7 @@ def main():
     timer_kernels = {"solve_light": ("solve_light", "solve_light16"),
                      "solve_heavy": ("solve_wave", "solve_heavy", "wave_partial", "heavy_partial", "heavy_reduce"),
                      "nnls_batch": ("nnls_batch",),
-                     "solve_nnls": ("solve_nnls", "heavy_partial", "heavy_reduce")}[dom]
+                     "solve_nnls": ("solve_nnls", "solve_nnls_row", "heavy_partial", "heavy_reduce")}[dom]
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json")
     if os.path.exists(tpath) and world == 1:
