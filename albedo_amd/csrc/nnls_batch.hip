@@ -69,8 +69,12 @@ struct NBatch {
   static constexpr int OFF_U = OFF_P + NW * SV * DLP;        // [SV][DLP]: Ỹv per slot
   static constexpr int AS = KP + 4;                          // A·lastDir row stride (banks)
   static constexpr int OFF_A = OFF_U + SV * DLP;             // [SV][AS]: A·lastDir per slot (fp32)
-  static constexpr int OFF_R = (OFF_A + SV * AS + 3) & ~3;   // doubles [2][NW][16][8]
-  static constexpr int OFF_C = OFF_R + 2 * 2 * NW * S * 8;      // ints: [0] refill base, [4 + j] slot j's row
+  static constexpr int OFF_R = (OFF_A + SV * AS + 3) & ~3;   // doubles [2][NW][16][RS]
+  // R: doubles [2][NW][16][RS]; RS = 9 (8 values + 1 pad): the slot stride of 18 dwords puts the 16
+  // slots' b64 accesses on 16 distinct bank pairs (at 8 they shared 4: the SQ counters of r06 showed
+  // 2.7 bank-conflict cycles per LDS instruction in this kernel)
+  static constexpr int RS = 9;
+  static constexpr int OFF_C = OFF_R + 2 * 2 * NW * S * RS;     // ints: [0] refill base, [4 + j] slot j's row
   static constexpr int FLOATS = OFF_C + 4 + S;
   static_assert(NW * RBW == NQ && NQ % 2 == 0 && RBW <= 2, "row blocks split evenly over the waves");
   static_assert(DL >= 1 && FLOATS * 4 <= 160 * 1024, "LDS");
@@ -167,10 +171,10 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
     constexpr int NSUM = decltype(NSUMC)::value, N = NSUM + decltype(NMAXC)::value;
 #pragma unroll
     for (int n = 0; n < N; ++n) v[n] = n < NSUM ? rows4<false>(v[n]) : rows4<true>(v[n]);
-    double* rp = R + buf * NW * S * 8 + off;
+    double* rp = R + buf * NW * S * NB::RS + off;
     if (g == 0) {
 #pragma unroll
-      for (int n = 0; n < N; ++n) rp[(w * S + j) * 8 + n] = v[n];
+      for (int n = 0; n < N; ++n) rp[(w * S + j) * NB::RS + n] = v[n];
     }
     __syncthreads();
     // readout split over the four lane groups: group g combines waves g·NW/4 .. of the slot's partials
@@ -179,10 +183,10 @@ __global__ __launch_bounds__((NBatch<KP, SV>::NTH), 1) void nnls_batch_kernel(So
     constexpr int WPG = NW / 4;
 #pragma unroll
     for (int n = 0; n < N; ++n) {
-      double t = rp[((WPG * g) * S + j) * 8 + n];
+      double t = rp[((WPG * g) * S + j) * NB::RS + n];
 #pragma unroll
       for (int u = 1; u < WPG; ++u)
-        t = n < NSUM ? t + rp[((WPG * g + u) * S + j) * 8 + n] : fmax(t, rp[((WPG * g + u) * S + j) * 8 + n]);
+        t = n < NSUM ? t + rp[((WPG * g + u) * S + j) * NB::RS + n] : fmax(t, rp[((WPG * g + u) * S + j) * NB::RS + n]);
       v[n] = n < NSUM ? rows4<false>(t) : rows4<true>(t);
     }
   };
