@@ -1601,16 +1601,20 @@ struct TopkPlan {
   int64_t n_chunks = 0, n_super = 0;
   bool prune = false;
   DevBuf d_th, d_keys, d_perm, d_nperm, d_tp, d_tmp, d_dstids, d_VP, d_cfeat, d_supf, d_probe, d_slab, d_G;
-  DevBuf d_src, d_ls, d_lc, d_flag, d_scan, d_okeys, d_order, d_srcs, d_otmp, d_thr, d_sf, d_mask, d_kth;
+  DevBuf d_scan;
+  // a pass's device buffers; two sets, so that a pass's select / rescans (on the post stream) can run
+  // while the next pass orders and scans with the other set (r06)
+  struct PassBufs {
+    DevBuf d_src, d_ls, d_lc, d_flag, d_okeys, d_order, d_srcs, d_otmp, d_thr, d_sf, d_mask, d_kth, d_inv;
+    DevBuf d_cnt;  // int [4]: the range's flagged count, the rescan work counter, the set's flagged total
+  } pb[2];
   // per call (topk_begin .. topk_finish): the passes run back to back with no host round trip; their
   // event pairs, scan counters (d_scan[pass]) and rows per scan workgroup are read at the end
-  DevBuf d_cnt;  // int [4]: this pass's flagged count, the rescan work counter, the call's flagged total
   // per pass: start, order + mask done, scan done, then per output range: select done, rescans done
   std::vector<hipEvent_t> evs;
   struct PassRec { int rpw; size_t e0; int ranges; };
   std::vector<PassRec> passes;
   int64_t n_passes = 0;
-  DevBuf d_inv;  // output slot -> scan position of the current pass
   hipError_t event(size_t i, hipEvent_t* e) {  // the i-th event of the pool (created on demand)
     while (evs.size() <= i) {
       hipEvent_t x;
@@ -1742,8 +1746,10 @@ static int64_t topk_pass_rows(als_ctx* c) {
 int topk_begin(als_ctx* c, TopkPlan& P, int64_t n_rows, int64_t n_passes, const int32_t* rows) {
   HIPCHK(P.d_scan.ensure((size_t)std::max<int64_t>(n_passes, 1) * 8));
   HIPCHK(hipMemsetAsync(P.d_scan.p, 0, (size_t)std::max<int64_t>(n_passes, 1) * 8, c->st));
-  HIPCHK(P.d_cnt.ensure(16));
-  HIPCHK(hipMemsetAsync(P.d_cnt.p, 0, 16, c->st));
+  for (auto& B : P.pb) {
+    HIPCHK(B.d_cnt.ensure(16));
+    HIPCHK(hipMemsetAsync(B.d_cnt.p, 0, 16, c->st));
+  }
   HIPCHK(c->d_last_need.ensure((size_t)std::max<int64_t>(n_rows, 1) * 4));
   HIPCHK(hipMemsetAsync(c->d_last_need.p, 0, (size_t)std::max<int64_t>(n_rows, 1) * 4, c->st));
   c->last_need_n = n_rows;
@@ -1758,13 +1764,16 @@ int topk_begin(als_ctx* c, TopkPlan& P, int64_t n_rows, int64_t n_passes, const 
   return ALS_OK;
 }
 
-int topk_finish(als_ctx* c, TopkPlan& P) {
+int topk_finish(als_ctx* c, TopkPlan& P, hipStream_t sp = nullptr) {
+  if (sp) HIPCHK(hipStreamSynchronize(sp));
   HIPCHK(hipStreamSynchronize(c->st));
   const int64_t np = (int64_t)P.passes.size();
   std::vector<unsigned long long> scanned((size_t)std::max<int64_t>(np, 1), 0ull);
-  int cnt[4] = {0, 0, 0, 0};
+  int cnt[4] = {0, 0, 0, 0}, cnt1[4] = {0, 0, 0, 0};
   if (np > 0) HIPCHK(copy_st(c, scanned.data(), P.d_scan.p, np * 8, hipMemcpyDeviceToHost));
-  HIPCHK(copy_st(c, cnt, P.d_cnt.p, 16, hipMemcpyDeviceToHost));
+  HIPCHK(copy_st(c, cnt, P.pb[0].d_cnt.p, 16, hipMemcpyDeviceToHost));
+  HIPCHK(copy_st(c, cnt1, P.pb[1].d_cnt.p, 16, hipMemcpyDeviceToHost));
+  cnt[2] += cnt1[2];
   for (int64_t q = 0; q < np; ++q) {
     const TopkPlan::PassRec& R = P.passes[q];
     const hipEvent_t* e = P.evs.data() + R.e0;
@@ -1790,23 +1799,28 @@ int topk_finish(als_ctx* c, TopkPlan& P) {
 // the caller can copy those rows out while the next range computes.
 using TopkReady = std::function<int(int64_t, int64_t)>;
 int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t row0, int64_t pos0, int64_t nc, int32_t* d_oid,
-                  float* d_osc, int64_t range = INT64_MAX, const TopkReady& ready = nullptr) {
+                  float* d_osc, int64_t range = INT64_MAX, const TopkReady& ready = nullptr, int par = 0,
+                  hipStream_t sp = nullptr) {
+  // buffer set `par`; with a post stream sp the select / rescans wait for the scan on sp, so the
+  // caller's next pass (the other set) can order and scan meanwhile
+  TopkPlan::PassBufs& B = P.pb[par];
+  hipStream_t ps = sp ? sp : c->st;
   Side& S = c->s[P.src];
   Side& T = c->s[1 - P.src];
   const int KP = c->KP, k = P.k;
   if (nc <= 0) return ALS_OK;
-  HIPCHK(P.d_src.ensure(nc * 4));
+  HIPCHK(B.d_src.ensure(nc * 4));
   if (!P.exact_only) {
-    HIPCHK(P.d_ls.ensure(nc * TOPK_CAP * 8));
-    HIPCHK(P.d_lc.ensure(nc * 4));
+    HIPCHK(B.d_ls.ensure(nc * TOPK_CAP * 8));
+    HIPCHK(B.d_lc.ensure(nc * 4));
   }
-  if (rows) HIPCHK(hipMemcpyAsync(P.d_src.p, rows, nc * 4, hipMemcpyHostToDevice, c->st));
-  else HIPCHK(launch_iota_i32(P.d_src.as<int32_t>(), nc, row0, c->st));
+  if (rows) HIPCHK(hipMemcpyAsync(B.d_src.p, rows, nc * 4, hipMemcpyHostToDevice, c->st));
+  else HIPCHK(launch_iota_i32(B.d_src.as<int32_t>(), nc, row0, c->st));
   (void)S;
   TopkArgs a{};
   a.S = S.d_orig.as<float>();
   a.T = T.d_orig.as<float>();
-  a.src_rows = P.d_src.as<int32_t>();
+  a.src_rows = B.d_src.as<int32_t>();
   a.n_src = nc;
   a.n_dst = T.n;
   a.dst_ids = P.d_dstids.as<int32_t>();
@@ -1824,8 +1838,8 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t row0, in
   a.tsc = (float)P.tsc;
   a.unscale = (float)(1.0 / (P.ssc * P.tsc));
   a.scaled = (float)(P.ssc * P.tsc);
-  a.lent = P.d_ls.as<uint2>();
-  a.lcnt = P.d_lc.as<int32_t>();
+  a.lent = B.d_ls.as<uint2>();
+  a.lcnt = B.d_lc.as<int32_t>();
   // scan order: 12 bits of depth, then 7 / 7 / 6 bits of direction (topk_order_key_kernel; c4 all
   // users: scan 260 -> 193 ms, order + mask 56 -> 39 ms against the depth-only key; 18 / 22 / 24
   // direction bits 206 / 206 / 276 ms, other splits of 20 the same 193)
@@ -1835,8 +1849,8 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t row0, in
   int32_t* d_need = c->d_last_need.as<int32_t>() + pos0;
   a.need_exact = d_need;
   if (!P.exact_only) {
-    HIPCHK(P.d_kth.ensure(nc * 4));
-    a.kth0 = P.d_kth.as<float>();
+    HIPCHK(B.d_kth.ensure(nc * 4));
+    a.kth0 = B.d_kth.as<float>();
   }
   const int64_t pass = (int64_t)P.passes.size();
   if (pass >= P.n_passes) return fail(ALS_E_STATE, "top-k: more passes than planned");
@@ -1854,37 +1868,38 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t row0, in
   // each row's results back to its own slot
   TopkArgs b = a;
   HIPCHK(hipEventRecord(ev[0], c->st));
-  HIPCHK(P.d_okeys.ensure(nc * 8));
-  HIPCHK(P.d_order.ensure(nc * 8));
-  HIPCHK(P.d_srcs.ensure(nc * 4));
+  HIPCHK(B.d_okeys.ensure(nc * 8));
+  HIPCHK(B.d_order.ensure(nc * 8));
+  HIPCHK(B.d_srcs.ensure(nc * 4));
   const size_t otb = topk_order_temp_bytes(nc);
-  HIPCHK(P.d_otmp.ensure(std::max<size_t>(otb, 16)));
-  HIPCHK(P.d_thr.ensure(nc * 8));
-  HIPCHK(P.d_sf.ensure((size_t)nc * TOPK_SF * 8));
-  float* sf_tmp = P.d_sf.as<float>();
+  HIPCHK(B.d_otmp.ensure(std::max<size_t>(otb, 16)));
+  HIPCHK(B.d_thr.ensure(nc * 8));
+  HIPCHK(B.d_sf.ensure((size_t)nc * TOPK_SF * 8));
+  float* sf_tmp = B.d_sf.as<float>();
   float* sf_sorted = sf_tmp + (size_t)nc * TOPK_SF;
-  HIPCHK(topk_order(KP, a, P.d_otmp.p, otb, P.d_okeys.as<uint32_t>(), P.d_order.as<uint32_t>(), P.d_srcs.as<int32_t>(),
-                    P.d_thr.as<float>(), P.d_thr.as<float>() + nc, sf_tmp, sf_sorted, c->st));
-  b.src_rows = P.d_srcs.as<int32_t>();
-  b.out_pos = P.d_order.as<uint32_t>();
-  b.thr0 = P.d_thr.as<float>() + nc;
+  HIPCHK(topk_order(KP, a, B.d_otmp.p, otb, B.d_okeys.as<uint32_t>(), B.d_order.as<uint32_t>(), B.d_srcs.as<int32_t>(),
+                    B.d_thr.as<float>(), B.d_thr.as<float>() + nc, sf_tmp, sf_sorted, c->st));
+  b.src_rows = B.d_srcs.as<int32_t>();
+  b.out_pos = B.d_order.as<uint32_t>();
+  b.thr0 = B.d_thr.as<float>() + nc;
   b.sfeat = sf_sorted;
   const int rpw = topk_rows_per_workgroup(KP, nc, c->n_cu);
   if (P.prune) {  // per scan workgroup, the chunks its rows can need against the starting thresholds
     const int64_t n_wg = (nc + rpw - 1) / rpw;
     b.mask_words = (P.n_super + 1) / 2;
-    HIPCHK(P.d_mask.ensure((size_t)n_wg * b.mask_words * 4));
-    b.mask = P.d_mask.as<uint32_t>();
-    HIPCHK(launch_topk_mask(b, rpw, P.d_supf.as<float>(), P.n_super, P.d_mask.as<uint32_t>(), c->st));
+    HIPCHK(B.d_mask.ensure((size_t)n_wg * b.mask_words * 4));
+    b.mask = B.d_mask.as<uint32_t>();
+    HIPCHK(launch_topk_mask(b, rpw, P.d_supf.as<float>(), P.n_super, B.d_mask.as<uint32_t>(), c->st));
   }
   HIPCHK(hipEventRecord(ev[1], c->st));
   HIPCHK(launch_topk(KP, b, c->n_cu, c->st));
   HIPCHK(hipEventRecord(ev[2], c->st));
+  HIPCHK(B.d_flag.ensure(nc * 4));
+  if (nr > 1) HIPCHK(B.d_inv.ensure(nc * 4));
+  if (sp) HIPCHK(hipStreamWaitEvent(sp, ev[2], 0));  // the select needs this pass's scan
   if (nr > 1) {  // select by output slot: slot -> scan position
-    HIPCHK(P.d_inv.ensure(nc * 4));
-    HIPCHK(launch_invert_perm(b.out_pos, nc, P.d_inv.as<uint32_t>(), c->st));
+    HIPCHK(launch_invert_perm(b.out_pos, nc, B.d_inv.as<uint32_t>(), ps));
   }
-  HIPCHK(P.d_flag.ensure(nc * 4));
   P.passes.push_back(TopkPlan::PassRec{rpw, e0, 0});
   for (int64_t r = 0; r < nr; ++r) {
     const int64_t o0 = r * range, n = std::min<int64_t>(range, nc - o0);
@@ -1893,12 +1908,12 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t row0, in
     HIPCHK(P.event(e0 + 4 + 2 * r, &ex));
     TopkArgs bs = b;
     if (nr > 1) {
-      bs.in_pos = P.d_inv.as<uint32_t>();
+      bs.in_pos = B.d_inv.as<uint32_t>();
       bs.slot0 = o0;
       bs.n_slots = n;
     }
-    HIPCHK(launch_topk_select(KP, bs, c->st));
-    HIPCHK(hipEventRecord(es, c->st));
+    HIPCHK(launch_topk_select(KP, bs, ps));
+    HIPCHK(hipEventRecord(es, ps));
     // certification failures of the range: compacted on the device (range-local positions), re-scored
     // in place
     TopkArgs ar = a;
@@ -1907,9 +1922,9 @@ int topk_run_rows(als_ctx* c, TopkPlan& P, const int32_t* rows, int64_t row0, in
     ar.out_scores = a.out_scores + o0 * k;
     ar.kth0 = a.kth0 + o0;
     ar.n_src = n;
-    HIPCHK(hipMemsetAsync(P.d_cnt.p, 0, 8, c->st));  // this range's count and work counter
-    HIPCHK(launch_topk_exact_flagged(KP, ar, d_need + o0, n, P.d_flag.as<int32_t>(), P.d_cnt.as<int>(), c->n_cu, c->st));
-    HIPCHK(hipEventRecord(ex, c->st));
+    HIPCHK(hipMemsetAsync(B.d_cnt.p, 0, 8, ps));  // this range's count and work counter
+    HIPCHK(launch_topk_exact_flagged(KP, ar, d_need + o0, n, B.d_flag.as<int32_t>(), B.d_cnt.as<int>(), c->n_cu, ps));
+    HIPCHK(hipEventRecord(ex, ps));
     P.passes.back().ranges = (int)(r + 1);
     if (ready) TRYC(ready(o0, o0 + n));
   }
@@ -1991,9 +2006,24 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   // five passes, 260 ms in one; profiles/r05_bench_c4_topk_pass{4M,10M,20M}.json).  The results are
   // finished and copied out in ranges of pass / 8 rows (at most 4M) while the next range computes.
   // ALBEDO_TOPK_PASS (test knob): rows per pass.
+  // ALBEDO_TOPK_OVERLAP=1 (r06 experiment, off by default): with the lists written in place the select
+  // is link-bound (~40 GB/s of lists) and the scan compute-bound, so a call of >= 2M rows runs as two
+  // passes whose first select / rescans (post stream, second buffer set) overlap the second order +
+  // scan.  Measured slower (c4 all users 0.318 vs 0.293 s, profiles/r06_bench_c4_topk_overlap_REJECTED
+  // .json): the store-bound select waves slow the concurrent scan, and the second pass adds its own
+  // order, sort and mask.
+  const bool want_overlap = [] {
+    const char* e = std::getenv("ALBEDO_TOPK_OVERLAP");
+    return e && std::atoi(e) == 1;
+  }();
   const int64_t chunk = [&] {
     const char* e = std::getenv("ALBEDO_TOPK_PASS");
-    return e && *e ? std::max<int64_t>(1 << 16, std::atoll(e)) : topk_pass_rows(c);
+    if (e && *e) return std::max<int64_t>(1 << 16, std::atoll(e));
+    const int64_t cap = topk_pass_rows(c);
+    const int64_t n_here = (std::min<int64_t>(n_known, ((int64_t)c->rank + 1) * ((n_known + c->world - 1) / c->world)) -
+                            std::min<int64_t>(n_known, (int64_t)c->rank * ((n_known + c->world - 1) / c->world)));
+    if (want_overlap && n_here >= ((int64_t)1 << 21)) return std::min<int64_t>(cap, (n_here + 1) / 2);
+    return cap;
   }();
   const int64_t range = std::min<int64_t>((int64_t)1 << 22, std::max<int64_t>(chunk / 8, 1 << 16));
   // world > 1 (SURVEY §8(e) "Top-k: shard users"): rank r scores the r-th contiguous slice of the
@@ -2080,7 +2110,17 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   std::vector<hipEvent_t> ev_rng;  // one per finished range: the copy stream waits for it
   DevBuf d_oid2[2], d_osc2[2];
   // releases everything the async path holds (null-safe: also after a partial set-up)
+  hipStream_t sp = nullptr;                   // the post stream of overlapped passes (zero-copy)
+  hipEvent_t ev_post[2] = {nullptr, nullptr};  // buffer set b's last select / rescans are done
+  auto end_post = [&]() {
+    if (sp) (void)hipStreamSynchronize(sp);
+    for (auto& e : ev_post)
+      if (e) (void)hipEventDestroy(e), e = nullptr;
+    if (sp) (void)hipStreamDestroy(sp);
+    sp = nullptr;
+  };
   auto end_async = [&]() {
+    end_post();
     if (!async_out) return;
     if (cs) (void)hipStreamSynchronize(cs);
     (void)hipStreamSynchronize(c->st);
@@ -2106,6 +2146,16 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
       (void)hipGetLastError();
     }
   }
+  if (async_out && zcopy && n_pass > 1) {  // a failure here leaves the passes sequential
+    bool ok = hipStreamCreateWithFlags(&sp, hipStreamNonBlocking) == hipSuccess;
+    if (!ok) sp = nullptr;
+    for (int b = 0; b < 2 && ok; ++b)
+      if (!(ok = hipEventCreateWithFlags(&ev_post[b], hipEventDisableTiming) == hipSuccess)) ev_post[b] = nullptr;
+    if (!ok) {
+      end_post();
+      (void)hipGetLastError();
+    }
+  }
   DevBuf d_oid, d_osc;
   {
     const int rc = topk_begin(c, P, n_known, n_pass, all_rows ? nullptr : known.data());
@@ -2117,9 +2167,15 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
   for (int64_t it = 0; it < n_pass; ++it) {
     const int64_t q0 = pstart[it], nc = (it + 1 < n_pass ? pstart[it + 1] : hi) - q0;
     if (async_out && zcopy) {  // results written in place by the kernels
-      // mode 2: select in output-slot order by ranges (consecutive waves write consecutive lists)
-      const int rc = topk_run_rows(c, P, rowsf(q0), q0, q0, nc, zids + (q0 - lo) * k, zsc + (q0 - lo) * k,
-                                   zmode == 2 ? range : INT64_MAX);
+      // mode 2: select in output-slot order by ranges (consecutive waves write consecutive lists);
+      // with a post stream, buffer set it & 1, reused once its previous select / rescans are done
+      const int par = sp ? (int)(it & 1) : 0;
+      int rc = ALS_OK;
+      if (sp && it >= 2 && hipStreamWaitEvent(c->st, ev_post[par], 0) != hipSuccess) rc = fail(ALS_E_HIP, "stream wait");
+      if (rc == ALS_OK)
+        rc = topk_run_rows(c, P, rowsf(q0), q0, q0, nc, zids + (q0 - lo) * k, zsc + (q0 - lo) * k,
+                           zmode == 2 ? range : INT64_MAX, nullptr, par, sp);
+      if (rc == ALS_OK && sp && hipEventRecord(ev_post[par], sp) != hipSuccess) rc = fail(ALS_E_HIP, "post event");
       if (rc != ALS_OK) {
         end_async();
         return rc;
@@ -2176,7 +2232,7 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
     }
   }
   {
-    const int rc = topk_finish(c, P);
+    const int rc = topk_finish(c, P, sp);
     if (rc != ALS_OK) {
       end_async();
       return rc;

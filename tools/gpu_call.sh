@@ -24,6 +24,7 @@ for s in "$@"; do
     tests_topk_zc) ALBEDO_TOPK_ZEROCOPY=1 timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_recommenders.py -k "topk or ndcg or recommend or transform or facade or albedo" > gpurun_out/tests_topk_zc.log 2>&1 ;;
     bench_trace_zc2) ALBEDO_TOPK_ZEROCOPY=2 ALBEDO_TOPK_TRACE=1 timeout -k 10 900 python -u bench.py --no-cpu > gpurun_out/bench_trace_zc2.json 2> gpurun_out/bench_trace_zc2.err ;;
     tests_topk_zc2) ALBEDO_TOPK_ZEROCOPY=2 timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_recommenders.py -k "topk or ndcg or recommend or transform or facade or albedo" > gpurun_out/tests_topk_zc2.log 2>&1 ;;
+    tests_c3_overlap) ALBEDO_TOPK_OVERLAP=1 timeout -k 10 600 $PYT tests/test_gpu_scale.py -s -k "c3_topk_passes" > gpurun_out/tests_c3_overlap.log 2>&1 ;;
     bench_c4) timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_c4.json 2> gpurun_out/bench_c4.err ;;
     bench_c2) timeout -k 10 300 python -u bench.py --config c2 --steps 10 --warmup 5 > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.err ;;
     bench_c5cpu) timeout -k 10 600 python -u bench.py --config c5 --steps 2 --warmup 1 --topk-users 0 > gpurun_out/bench_c5cpu.json 2> gpurun_out/bench_c5cpu.err ;;
