@@ -1663,12 +1663,16 @@ int topk_dst_basis(als_ctx* c, const Side& T, TopkPlan& P, std::vector<double>& 
 // 12 / 16 / 24 -> 33.6 / 47.6 / 50.7 / 46.9M users/s; fewer leave more rows to the exact rescan)
 int topk_threshold_rank(int k) { return std::max(k, std::min(TOPK_KC, k + ALBEDO_TOPK_KT_EXTRA)); }
 
-int topk_plan(als_ctx* c, int src, int k, TopkPlan& P) {
+int topk_plan(als_ctx* c, int src, int k, TopkPlan& P, const std::function<void(const char*)>& stamp = nullptr) {
+  auto st = [&](const char* w) {
+    if (stamp) stamp(w);
+  };
   P.src = src;
   P.k = k;
   P.exact_only = k > TOPK_KC;  // no MFMA pre-selection: exact full scan of every row
   TRYC(materialize(c, src));
   TRYC(materialize(c, 1 - src));
+  st("  plan: materialize dst");
   Side& S = c->s[src];
   Side& T = c->s[1 - src];
   const int KP = c->KP;
@@ -1701,8 +1705,10 @@ int topk_plan(als_ctx* c, int src, int k, TopkPlan& P) {
   // the chunk bound prunes only catalogues larger than the candidate lists (smaller ones are scanned
   // whole: the lists then hold every dst row, which select's n_dst <= TOPK_KC shortcut relies on)
   P.prune = T.n > TOPK_KC;
+  st("  plan: row norms");
   std::vector<double> VP;
   TRYC(topk_dst_basis(c, T, P, VP));
+  st("  plan: dst Gram + host eigensolve");
   HIPCHK(P.d_VP.ensure(VP.size() * 8));
   HIPCHK(hipMemcpyAsync(P.d_VP.p, VP.data(), VP.size() * 8, hipMemcpyHostToDevice, c->st));
   const int64_t nn = std::max<int64_t>(T.n, 1);
@@ -1721,9 +1727,11 @@ int topk_plan(als_ctx* c, int src, int k, TopkPlan& P) {
                         P.d_keys.as<uint32_t>(), P.d_perm.as<uint32_t>(), P.d_nperm.as<uint32_t>(),
                         P.d_tp.as<double>(), P.d_th.p, P.d_cfeat.as<float>(), P.d_supf.as<float>(), P.d_probe.p,
                         c->st));
+  st("  plan: dst sort + fp16 pack + chunk features");
   HIPCHK(P.d_dstids.ensure(std::max<int64_t>(T.n, 1) * 4));
   HIPCHK(hipMemcpyAsync(P.d_dstids.p, T.ids.data(), T.n * 4, hipMemcpyHostToDevice, c->st));
   HIPCHK(P.d_scan.ensure(8));
+  st("  plan: dst ids");
   return ALS_OK;
 }
 
@@ -2078,7 +2086,7 @@ int als_recommend(als_ctx* c, int side, int32_t k, const int32_t* subset, int64_
     }
   }
   TopkPlan P;
-  const int plan_rc = topk_plan(c, src, k, P);
+  const int plan_rc = topk_plan(c, src, k, P, trace ? std::function<void(const char*)>(stamp) : nullptr);
   if (pin_thr.joinable()) pin_thr.join();
   (void)hipGetLastError();  // a refused registration is not an error: the synchronous path runs
   if (pin_state == 1) (void)hipHostUnregister(dst_ids_out + lo * k);
