@@ -50,6 +50,11 @@ def main():
             return 0
 
         ar, ag = L.ALLREDUCE_FN(allreduce), L.ALLGATHER_FN(allgather)
+        if os.environ.get("ALBEDO_TEST_POLLUTE"):  # tools/repro_mrbig.py: leave NaN-filled freed memory
+            junk = torch.full((int(os.environ["ALBEDO_TEST_POLLUTE"]) << 28,), float("nan"), device="cuda")
+            torch.cuda.synchronize()
+            del junk
+            torch.cuda.empty_cache()
         p = L.als_params()
         L.check(lib.als_params_default(C.byref(p)))
         p.rank, p.implicit_prefs, p.reg_param, p.alpha, p.max_iter = k, 1, 0.5, 40.0, 1 if big else 3

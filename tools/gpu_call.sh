@@ -29,6 +29,7 @@ for s in "$@"; do
     bench_c2) timeout -k 10 300 python -u bench.py --config c2 --steps 10 --warmup 5 > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.err ;;
     bench_c5cpu) timeout -k 10 600 python -u bench.py --config c5 --steps 2 --warmup 1 --topk-users 0 > gpurun_out/bench_c5cpu.json 2> gpurun_out/bench_c5cpu.err ;;
     bench_c5_s*) ALBEDO_NNLS_MIN_SLOTS=${s#bench_c5_s} timeout -k 10 400 python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/$s.json 2> gpurun_out/$s.err ;;
+    repro_mrbig) timeout -k 10 600 python -u tools/repro_mrbig.py 16 /tmp/repro_mrbig > gpurun_out/repro_mrbig.log 2>&1 ;;
     tests_mrbig) timeout -k 10 900 $PYT tests/test_multi_rank.py -k c4_shaped > gpurun_out/tests_mrbig.log 2>&1 ;;
     batchtime4) (cd tools/probe && timeout -k 5 120 ./batchtime 256 16 500000 200000 6 && timeout -k 5 120 ./batchtime 256 8 500000 100000 12 && timeout -k 5 120 ./batchtime 256 4 500000 50000 24) > gpurun_out/batchtime4.txt 2>&1 ;;
     bench_c5) timeout -k 10 400 python -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu --topk-users 0 > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err ;;
