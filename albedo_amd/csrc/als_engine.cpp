@@ -1631,17 +1631,29 @@ struct TopkPlan {
   }
 };
 
-// The leading TOPK_M eigenvectors of the dst side's Gram Σ t tᵀ (original basis), fp64 [TOPK_M][KP]:
-// the directions the top-k chunk bound keeps exactly (topk.hip).
-int topk_dst_basis(als_ctx* c, const Side& T, TopkPlan& P, std::vector<double>& VP) {
-  const int KP = c->KP, k = c->p.rank;
+// The dst side's Gram Σ t tᵀ (original basis) on the device, copied into Gf ([KP][KP] fp64) on st;
+// `done` is recorded behind the copy, so the host can wait for it alone.
+int topk_dst_gram(als_ctx* c, const Side& T, TopkPlan& P, std::vector<double>& Gf, hipEvent_t done) {
+  const int KP = c->KP;
   const int nblk = gram_slab_blocks(KP, T.n);
-  HIPCHK(P.d_slab.ensure(gram_slab_doubles(KP, nblk) * 8));
+  double* slab = c->slab.as<double>();  // the sweeps' Gram scratch (idle here, same stream) when it fits
+  if (c->slab_blocks < nblk || !slab) {
+    HIPCHK(P.d_slab.ensure(gram_slab_doubles(KP, nblk) * 8));
+    slab = P.d_slab.as<double>();
+  }
   HIPCHK(P.d_G.ensure((size_t)KP * KP * 8));
-  HIPCHK(launch_gram(KP, T.d_orig.as<float>(), T.n, P.d_slab.as<double>(), nblk, P.d_G.as<double>(), c->st));
-  std::vector<double> Gf((size_t)KP * KP), Gk((size_t)k * k), w(k), V((size_t)k * k);
+  HIPCHK(launch_gram(KP, T.d_orig.as<float>(), T.n, slab, nblk, P.d_G.as<double>(), c->st));
+  Gf.assign((size_t)KP * KP, 0.0);
   HIPCHK(hipMemcpyAsync(Gf.data(), P.d_G.p, Gf.size() * 8, hipMemcpyDeviceToHost, c->st));
-  HIPCHK(hipStreamSynchronize(c->st));
+  HIPCHK(hipEventRecord(done, c->st));
+  return ALS_OK;
+}
+
+// The leading TOPK_M eigenvectors of that Gram, fp64 [TOPK_M][KP]: the directions the top-k chunk
+// bound keeps exactly (topk.hip).  Runs on the host while the row norms are computed on the device.
+int topk_dst_basis(als_ctx* c, const std::vector<double>& Gf, std::vector<double>& VP) {
+  const int KP = c->KP, k = c->p.rank;
+  std::vector<double> Gk((size_t)k * k), w(k), V((size_t)k * k);
   for (int i = 0; i < k; ++i)
     for (int j = 0; j < k; ++j) Gk[(size_t)i * k + j] = Gf[(size_t)i * KP + j];
   if (!sym_eig(k, Gk.data(), w.data(), V.data()))
@@ -1676,6 +1688,11 @@ int topk_plan(als_ctx* c, int src, int k, TopkPlan& P, const std::function<void(
   Side& S = c->s[src];
   Side& T = c->s[1 - src];
   const int KP = c->KP;
+  // the dst Gram first; its host eigensolve overlaps the row-norm launches behind it
+  std::vector<double> Gf, VP;
+  hipEvent_t ev_gram;
+  HIPCHK(P.event(0, &ev_gram));
+  TRYC(topk_dst_gram(c, T, P, Gf, ev_gram));
   {
     DevBuf d_nrm;
     HIPCHK(d_nrm.ensure(16));
@@ -1683,6 +1700,10 @@ int topk_plan(als_ctx* c, int src, int k, TopkPlan& P, const std::function<void(
     HIPCHK(launch_rownorm_max(S.d_orig.as<float>(), S.n, KP, c->p.rank, d_nrm.as<unsigned long long>() + 1, c->st));
     double nr[2];
     HIPCHK(hipMemcpyAsync(nr, d_nrm.p, 16, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipEventSynchronize(ev_gram));
+    st("  plan: dst Gram");
+    TRYC(topk_dst_basis(c, Gf, VP));
+    st("  plan: host eigensolve (row norms on the device)");
     HIPCHK(hipStreamSynchronize(c->st));
     P.tmax = nr[0];
     P.smax = nr[1];
@@ -1706,9 +1727,6 @@ int topk_plan(als_ctx* c, int src, int k, TopkPlan& P, const std::function<void(
   // whole: the lists then hold every dst row, which select's n_dst <= TOPK_KC shortcut relies on)
   P.prune = T.n > TOPK_KC;
   st("  plan: row norms");
-  std::vector<double> VP;
-  TRYC(topk_dst_basis(c, T, P, VP));
-  st("  plan: dst Gram + host eigensolve");
   HIPCHK(P.d_VP.ensure(VP.size() * 8));
   HIPCHK(hipMemcpyAsync(P.d_VP.p, VP.data(), VP.size() * 8, hipMemcpyHostToDevice, c->st));
   const int64_t nn = std::max<int64_t>(T.n, 1);
