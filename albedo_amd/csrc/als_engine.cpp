@@ -183,6 +183,7 @@ struct als_ctx {
   // rescanned when d_last_need[p] != 0; its src row is p (last_rows_dense) or last_rows[p]
   mutable std::vector<int32_t> last_rescan;
   DevBuf d_last_need;
+  double* h_plan = nullptr;      // pinned: the top-k plan's dst Gram [KP][KP] + two max row norms
   int64_t last_need_n = 0;
   std::vector<int32_t> last_rows;
   mutable bool last_rescan_ready = true;
@@ -1335,6 +1336,7 @@ static void destroy_now(als_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->evt)
     if (e) (void)hipEventDestroy(e);
+  if (c->h_plan) (void)hipHostFree(c->h_plan);
   if (c->st2) (void)hipStreamDestroy(c->st2);
   if (c->st) (void)hipStreamDestroy(c->st);
   delete c;
@@ -1631,9 +1633,9 @@ struct TopkPlan {
   }
 };
 
-// The dst side's Gram Σ t tᵀ (original basis) on the device, copied into Gf ([KP][KP] fp64) on st;
-// `done` is recorded behind the copy, so the host can wait for it alone.
-int topk_dst_gram(als_ctx* c, const Side& T, TopkPlan& P, std::vector<double>& Gf, hipEvent_t done) {
+// The dst side's Gram Σ t tᵀ (original basis) on the device, copied into c->h_plan ([KP][KP] fp64)
+// on st; `done` is recorded behind the copy, so the host can wait for it alone.
+int topk_dst_gram(als_ctx* c, const Side& T, TopkPlan& P, hipEvent_t done) {
   const int KP = c->KP;
   const int nblk = gram_slab_blocks(KP, T.n);
   double* slab = c->slab.as<double>();  // the sweeps' Gram scratch (idle here, same stream) when it fits
@@ -1643,15 +1645,15 @@ int topk_dst_gram(als_ctx* c, const Side& T, TopkPlan& P, std::vector<double>& G
   }
   HIPCHK(P.d_G.ensure((size_t)KP * KP * 8));
   HIPCHK(launch_gram(KP, T.d_orig.as<float>(), T.n, slab, nblk, P.d_G.as<double>(), c->st));
-  Gf.assign((size_t)KP * KP, 0.0);
-  HIPCHK(hipMemcpyAsync(Gf.data(), P.d_G.p, Gf.size() * 8, hipMemcpyDeviceToHost, c->st));
+  // into pinned memory: a pageable copy would block the host here until the stream drains
+  HIPCHK(hipMemcpyAsync(c->h_plan, P.d_G.p, (size_t)KP * KP * 8, hipMemcpyDeviceToHost, c->st));
   HIPCHK(hipEventRecord(done, c->st));
   return ALS_OK;
 }
 
 // The leading TOPK_M eigenvectors of that Gram, fp64 [TOPK_M][KP]: the directions the top-k chunk
 // bound keeps exactly (topk.hip).  Runs on the host while the row norms are computed on the device.
-int topk_dst_basis(als_ctx* c, const std::vector<double>& Gf, std::vector<double>& VP) {
+int topk_dst_basis(als_ctx* c, const double* Gf, std::vector<double>& VP) {
   const int KP = c->KP, k = c->p.rank;
   std::vector<double> Gk((size_t)k * k), w(k), V((size_t)k * k);
   for (int i = 0; i < k; ++i)
@@ -1689,20 +1691,22 @@ int topk_plan(als_ctx* c, int src, int k, TopkPlan& P, const std::function<void(
   Side& T = c->s[1 - src];
   const int KP = c->KP;
   // the dst Gram first; its host eigensolve overlaps the row-norm launches behind it
-  std::vector<double> Gf, VP;
+  std::vector<double> VP;
   hipEvent_t ev_gram;
   HIPCHK(P.event(0, &ev_gram));
-  TRYC(topk_dst_gram(c, T, P, Gf, ev_gram));
+  if (!c->h_plan) HIPCHK(hipHostMalloc((void**)&c->h_plan, ((size_t)KP * KP + 2) * 8, hipHostMallocDefault));
   {
     DevBuf d_nrm;
     HIPCHK(d_nrm.ensure(16));
+    TRYC(topk_dst_gram(c, T, P, ev_gram));
     HIPCHK(launch_rownorm_max(T.d_orig.as<float>(), T.n, KP, c->p.rank, d_nrm.as<unsigned long long>(), c->st));
     HIPCHK(launch_rownorm_max(S.d_orig.as<float>(), S.n, KP, c->p.rank, d_nrm.as<unsigned long long>() + 1, c->st));
-    double nr[2];
+    double* nr = c->h_plan + (size_t)KP * KP;
     HIPCHK(hipMemcpyAsync(nr, d_nrm.p, 16, hipMemcpyDeviceToHost, c->st));
+    st("  plan: dst Gram + row norms enqueued");
     HIPCHK(hipEventSynchronize(ev_gram));
     st("  plan: dst Gram");
-    TRYC(topk_dst_basis(c, Gf, VP));
+    TRYC(topk_dst_basis(c, c->h_plan, VP));
     st("  plan: host eigensolve (row norms on the device)");
     HIPCHK(hipStreamSynchronize(c->st));
     P.tmax = nr[0];
